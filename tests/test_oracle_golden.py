@@ -1,0 +1,181 @@
+"""Pin the CPU oracle to the reference: every golden vector produced by the
+reference dislib (tests/golden/gen_golden.py) must be reproduced bit-exactly.
+CPU only."""
+import hashlib
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+from sklearn.datasets import make_blobs
+
+from oracle import kmeans_oracle as orc
+from tests.conftest import load_golden
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _blocks(x, subset_size):
+    return [x[i:i + subset_size] for i in range(0, x.shape[0], subset_size)]
+
+
+def _fit(x, subset_size, set_labels=True, sparse=False, **kw):
+    m = orc.OracleKMeans(**kw)
+    lab = m.fit(_blocks(x, subset_size), sparse=sparse, set_labels=set_labels)
+    return m, lab
+
+
+def test_f01_toy_integer_fit_and_predict():
+    g = load_golden("f01_toy")
+    x = np.array([[1, 2], [2, 1], [-1, -2], [-2, -1]])
+    m = orc.OracleKMeans(n_clusters=2, random_state=666)
+    m.fit([x[:2], x[2:]])
+    assert np.array_equal(m.centers, g["centers"])
+    assert np.array_equal(m.centers, [[1.5, 1.5], [-1.5, -1.5]])
+    assert m.n_iter == g["n_iter"]
+    test = np.array([[1, 2], [2, 1], [-1, -2], [-2, -1], [10, 10], [-10, -10]])
+    pred = m.predict(_blocks(test, 2))
+    assert np.array_equal(pred, g["predict_labels"])
+
+
+def test_f03_blobs610_bit_exact():
+    g = load_golden("f03_blobs610")
+    x, y = make_blobs(n_samples=1500, random_state=170)
+    xf = np.vstack((x[y == 0][:500], x[y == 1][:100], x[y == 2][:10]))
+    assert np.array_equal(xf, g["x"])
+    m, lab = _fit(xf, 300, n_clusters=3, random_state=170)
+    # the reference's own literal pin, tests/test_kmeans.py:78-82
+    lit = np.array([[-8.941375656533449, -5.481371322614891],
+                    [-4.524023204953875, 0.06235042593214654],
+                    [2.332994701667008, 0.37681003933082696]])
+    assert (m.centers == lit).all()
+    assert np.array_equal(m.centers, g["centers"])
+    assert np.array_equal(lab, g["labels"])
+    assert m.n_iter == g["n_iter"]
+    assert np.array_equal(np.array(m.trace), g["trace"])
+
+
+@pytest.mark.parametrize("name,n,d,blobs,box,rs,sub,k,iters", [
+    ("f04_c1mini", 20000, 50, 10, None, 0, 2000, 10, 5),
+    ("f05_c2mini", 20000, 32, 100, (-10, 10), 1, 5000, 100, 3),
+    ("f06_c3mini", 10000, 64, 50, (-10, 10), 2, 5000, 1000, 2),
+])
+def test_config_minis_bit_exact(name, n, d, blobs, box, rs, sub, k, iters):
+    g = load_golden(name)
+    kw = dict(n_samples=n, n_features=d, centers=blobs, random_state=rs)
+    if box is not None:
+        kw["center_box"] = box
+    x, _ = make_blobs(**kw)
+    assert _sha(x) == str(g["x_sha"])
+    m, lab = _fit(x, sub, n_clusters=k, max_iter=iters, tol=0, random_state=0)
+    assert m.n_iter == g["n_iter"]
+    assert np.array_equal(np.array(m.trace), g["trace"])
+    assert np.array_equal(lab, g["labels"])
+
+
+def test_f07_sparse_and_dense():
+    g = load_golden("f07_sparse")
+    xs = sp.csr_matrix((g["data"], g["indices"], g["indptr"]),
+                       shape=tuple(g["shape"]))
+    m, lab = _fit(xs, 200, sparse=True, n_clusters=8, random_state=170)
+    assert m.n_iter == g["sparse_n_iter"]
+    assert np.array_equal(lab, g["sparse_labels"])
+    assert np.array_equal(np.array(m.trace), g["sparse_trace"])
+    assert np.array_equal(m.predict(_blocks(xs, 500), sparse=True),
+                          g["sparse_predict"])
+    md, labd = _fit(xs.toarray(), 200, n_clusters=8, random_state=170)
+    assert np.array_equal(np.array(md.trace), g["dense_trace"])
+    assert np.array_equal(labd, g["dense_labels"])
+    # the reference's own sparse-vs-dense claim (tests/test_kmeans.py:100-101)
+    assert np.allclose(g["sparse_centers"], g["dense_centers"])
+
+
+def test_f08_ties_first_index():
+    g = load_golden("f08_ties")
+    lab = orc.predict_labels(g["exact_x"], g["exact_c"])
+    assert np.array_equal(lab, g["exact_labels"])
+    for x0, cc, want in zip(g["sqrt_x"], g["sqrt_c"], g["sqrt_labels"]):
+        assert orc.predict_labels(x0[None], cc)[0] == want == 0
+        # the constructed pair really is a sqrt tie with s_a > s_b
+        sa = orc.pairwise_sum((x0 - cc[0]) ** 2)
+        sb = orc.pairwise_sum((x0 - cc[1]) ** 2)
+        assert sa > sb and np.sqrt(sa) == np.sqrt(sb)
+    assert np.array_equal(orc.predict_labels(g["near_x"], g["near_c"]),
+                          g["near_labels"])
+
+
+def test_f09_empty_clusters_keep_init():
+    g = load_golden("f09_empty")
+    m, lab = _fit(g["x"], 50, n_clusters=6, max_iter=4, random_state=9)
+    assert np.array_equal(m.centers, g["centers"])
+    assert np.array_equal(lab, g["labels"])
+    init = orc.init_centers(2, False, 6, 9)
+    empty = np.setdiff1d(np.arange(6), lab)
+    assert len(empty) > 0
+    assert np.array_equal(m.centers[empty], init[empty])
+
+
+def test_f10_fp32_samples():
+    g = load_golden("f10_fp32")
+    m, lab = _fit(g["x"], 500, n_clusters=4, max_iter=5, tol=0, random_state=3)
+    assert np.array_equal(np.array(m.trace), g["trace"])
+    assert np.array_equal(lab, g["labels"])
+
+
+def test_f11_iteration_count_rules(capsys):
+    g = load_golden("f11_iters")
+    m, _ = _fit(g["x"], 100, set_labels=False, n_clusters=3, max_iter=0,
+                random_state=11)
+    assert m.n_iter == g["n_iter_max0"] == 1
+    assert np.array_equal(m.centers, g["centers_max0"])
+    m, _ = _fit(g["x"], 100, set_labels=False, n_clusters=3, max_iter=50,
+                tol=1e-1, random_state=11, verbose=True)
+    assert m.n_iter == g["n_iter_tol"]
+    assert np.array_equal(m.centers, g["centers_tol"])
+    out = capsys.readouterr().out
+    want = str(g["verbose"])
+    # printed criterion uses BLAS dot; compare the line structure + iteration
+    assert [l.split("=")[0] for l in out.splitlines()] == \
+        [l.split("=")[0] for l in want.splitlines()]
+
+
+def test_f12_fit_predict_labels_are_last_assignment():
+    g = load_golden("f12_lastassign")
+    m, lab = _fit(g["x"], 250, n_clusters=5, max_iter=2, tol=0, random_state=7)
+    assert np.array_equal(lab, g["fit_predict"])
+    assert np.array_equal(m.predict(_blocks(g["x"], 250)), g["predict"])
+    assert not np.array_equal(g["fit_predict"], g["predict"])
+
+
+@pytest.mark.parametrize("arity", [50, 2])
+def test_f13_merge_tree_order(arity):
+    g = load_golden("f13_arity")
+    m, lab = _fit(g["x"], 50, n_clusters=6, max_iter=4, tol=0, arity=arity,
+                  random_state=13)
+    assert np.array_equal(np.array(m.trace), g["trace_a%d" % arity])
+    assert np.array_equal(lab, g["labels_a%d" % arity])
+
+
+def test_pairwise_sum_model_matches_numpy():
+    rng = np.random.default_rng(5)
+    for d in [1, 2, 7, 8, 9, 16, 31, 50, 64, 127, 128, 129, 200, 1000, 1024,
+              8200, 10000]:
+        x = rng.standard_normal(d) * 7
+        C = rng.random((3, d))
+        ref = orc.vec_matrix_euclid(x, C)
+        mod = np.array([np.sqrt(orc.pairwise_sum((x - c) ** 2)) for c in C])
+        assert np.array_equal(ref, mod), d
+        assert np.array_equal(orc.dense_distances(x[None], C)[0], ref), d
+
+
+def test_init_centers_rejects_randomstate():
+    with pytest.raises(TypeError):
+        orc.init_centers(2, False, 2, np.random.RandomState(0))
+
+
+def test_synthetic_blobs_generator_is_row_addressable():
+    a, la = orc.make_blobs_rows(0, 100, 5, 7, seed=3)
+    b, lb = orc.make_blobs_rows(40, 20, 5, 7, seed=3)
+    assert np.array_equal(a[40:60], b) and np.array_equal(la[40:60], lb)
+    assert np.isfinite(a).all() and 0 <= la.min() and la.max() < 7
