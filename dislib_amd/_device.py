@@ -1,0 +1,215 @@
+"""Device residency and thin launch wrappers around ``libdkm.so``.
+
+PyTorch is used only as the device allocator / stream provider: tensors are
+HBM buffers whose ``data_ptr()`` goes through the C ABI.  All compute is in
+the HIP kernels of ``dislib_amd/csrc``.
+
+``DeviceData`` is the HBM image of a :class:`dislib_amd.data.Dataset`: every
+Subset's rows concatenated into one row-major matrix (or one CSR matrix),
+with the Subset boundaries kept as row offsets.  It replaces PyCOMPSs'
+per-task pickling of Subsets (reference ``cluster/kmeans/base.py:113-115``,
+``data/classes.py:298-304``): the data is uploaded once and stays resident
+for every Lloyd iteration.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+
+def torch():
+    import torch as _t
+    return _t
+
+
+def stream_ptr():
+    t = torch()
+    return ctypes.c_void_p(t.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class DeviceData:
+    """HBM image of a Dataset (dense or CSR)."""
+
+    def __init__(self, dataset, device=None):
+        t = torch()
+        self.device = t.device(device if device is not None else "cuda")
+        subsets = list(dataset)
+        self.sizes = [int(s.samples.shape[0]) for s in subsets]
+        self.offsets = np.concatenate([[0], np.cumsum(self.sizes)]).astype(
+            np.int64)
+        self.n = int(self.offsets[-1])
+        self.d = int(dataset.n_features)
+        self.sparse = bool(dataset.sparse)
+        if self.sparse:
+            self._upload_csr(subsets)
+        else:
+            self._upload_dense(subsets)
+
+    # -- dense -------------------------------------------------------------
+    def _upload_dense(self, subsets):
+        t = torch()
+        dev_parts = [s.samples for s in subsets
+                     if _is_torch(s.samples)]
+        if dev_parts and len(dev_parts) == len(subsets):
+            # already device-resident (e.g. bench data): view/concat on device
+            xs = [s.samples for s in subsets]
+            dt = xs[0].dtype
+            self.dtype = np.float32 if dt == t.float32 else np.float64
+            X = _adjacent_view(xs)
+            if X is None:
+                X = xs[0] if len(xs) == 1 else t.cat(xs, 0)
+            self.X = X.to(self.device, dtype=(t.float32 if self.dtype ==
+                                             np.float32 else t.float64))
+            self.X = self.X.contiguous()
+            return
+        arrs = [np.asarray(s.samples) for s in subsets]
+        dts = {a.dtype for a in arrs}
+        if dts == {np.dtype(np.float32)}:
+            self.dtype = np.float32
+        else:
+            # fp64 samples; integer samples are exact in fp64 below 2**53
+            self.dtype = np.float64
+        host = np.concatenate([a.astype(self.dtype, copy=False)
+                               for a in arrs]) if arrs else \
+            np.zeros((0, self.d), self.dtype)
+        host = np.ascontiguousarray(host.reshape(self.n, self.d))
+        self.X = t.from_numpy(host).to(self.device)
+        self.int_input = any(np.issubdtype(a.dtype, np.integer) for a in arrs)
+
+    # -- CSR ---------------------------------------------------------------
+    def _upload_csr(self, subsets):
+        import scipy.sparse as sp
+        t = torch()
+        mats = [sp.csr_matrix(s.samples) for s in subsets]
+        m = sp.vstack(mats, format="csr") if mats else \
+            sp.csr_matrix((0, self.d))
+        # keep each row's stored order: it is the reference's dot order
+        self.dtype = np.float64
+        self.indptr = t.from_numpy(m.indptr.astype(np.int64)).to(self.device)
+        self.indices = t.from_numpy(m.indices.astype(np.int32)).to(
+            self.device)
+        self.data = t.from_numpy(m.data.astype(np.float64)).to(self.device)
+
+    # -- helpers -----------------------------------------------------------
+    def subset_slices(self):
+        return [(int(a), int(b)) for a, b in zip(self.offsets[:-1],
+                                                 self.offsets[1:])]
+
+
+def _adjacent_view(xs):
+    """One (n, d) view over row blocks that are consecutive slices of one
+    device buffer (e.g. ``load_data`` of a device tensor): no copy."""
+    t = torch()
+    x0 = xs[0]
+    if x0.dim() != 2 or x0.stride(1) != 1:
+        return None
+    ld, es = x0.stride(0), x0.element_size()
+    nxt = x0.data_ptr()
+    for x in xs:
+        if (x.dim() != 2 or x.dtype != x0.dtype or x.stride(1) != 1 or
+                x.shape[1] != x0.shape[1] or
+                (x.shape[0] > 1 and x.stride(0) != ld) or
+                x.data_ptr() != nxt or x.device != x0.device):
+            return None
+        nxt += x.shape[0] * ld * es
+    n = sum(int(x.shape[0]) for x in xs)
+    return t.as_strided(x0, (n, x0.shape[1]), (ld, 1))
+
+
+def _is_torch(x):
+    try:
+        import torch as _t
+        return isinstance(x, _t.Tensor)
+    except ImportError:          # pragma: no cover
+        return False
+
+
+class Workspace:
+    """Caller-owned scratch for the C ABI (``dkm_workspace_bytes``)."""
+
+    def __init__(self, k, d, n_queue, device):
+        t = torch()
+        so = _lib.lib()
+        self.k, self.d = int(k), int(d)
+        self.nbytes = int(so.dkm_workspace_bytes(self.k, self.d,
+                                                 int(n_queue)))
+        if self.nbytes == 0:
+            raise _lib.DkmError("dkm_workspace_bytes: bad k/d")
+        self.buf = t.zeros(self.nbytes, dtype=t.uint8, device=device)
+
+    @property
+    def p(self):
+        return ctypes.c_void_p(self.buf.data_ptr())
+
+
+# ---------------------------------------------------------------------------
+# launch wrappers (all stream-ordered on torch's current stream)
+# ---------------------------------------------------------------------------
+def prepare(C, ws, acc, csr=False):
+    so = _lib.lib()
+    k, d = C.shape
+    _lib.check(so.dkm_prepare_centers(ptr(C), k, d,
+                                      _lib.PREP_CSR if csr else 0, ws.p,
+                                      ws.nbytes, ptr(acc), stream_ptr()),
+               "dkm_prepare_centers")
+
+
+def partial_sum(dd, C, ws, labels, acc, mode):
+    so = _lib.lib()
+    k = C.shape[0]
+    if dd.sparse:
+        _lib.check(so.dkm_partial_sum_csr_f64(
+            ptr(dd.indptr), ptr(dd.indices), ptr(dd.data), dd.n, dd.d,
+            ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(acc), stream_ptr()),
+            "dkm_partial_sum_csr_f64")
+        return
+    fn = so.dkm_partial_sum_f32 if dd.dtype == np.float32 else \
+        so.dkm_partial_sum_f64
+    _lib.check(fn(ptr(dd.X), dd.n, dd.d, dd.X.stride(0), ptr(C), k, ws.p,
+                  ws.nbytes, ptr(labels), ptr(acc), mode, stream_ptr()),
+               "dkm_partial_sum")
+
+
+def predict(dd, C, ws, labels, mode):
+    so = _lib.lib()
+    k = C.shape[0]
+    if dd.sparse:
+        _lib.check(so.dkm_predict_csr_f64(
+            ptr(dd.indptr), ptr(dd.indices), ptr(dd.data), dd.n, dd.d,
+            ptr(C), k, ws.p, ws.nbytes, ptr(labels), stream_ptr()),
+            "dkm_predict_csr_f64")
+        return
+    fn = so.dkm_predict_f32 if dd.dtype == np.float32 else so.dkm_predict_f64
+    _lib.check(fn(ptr(dd.X), dd.n, dd.d, dd.X.stride(0), ptr(C), k, ws.p,
+                  ws.nbytes, ptr(labels), mode, stream_ptr()),
+               "dkm_predict")
+
+
+def update(acc, C, sums_mode, tol, diff, flag):
+    so = _lib.lib()
+    k, d = C.shape
+    _lib.check(so.dkm_update_centers(ptr(acc), ptr(C), k, d, sums_mode,
+                                     float(tol), ptr(diff), ptr(flag),
+                                     stream_ptr()), "dkm_update_centers")
+
+
+def make_blobs(X, row0, n_blobs, seed, box=10.0, std=1.0, blob=None):
+    so = _lib.lib()
+    n, d = X.shape
+    _lib.check(so.dkm_make_blobs_f64(ptr(X), int(row0), n, d, int(n_blobs),
+                                     int(seed), float(box), float(std),
+                                     ptr(blob), stream_ptr()),
+               "dkm_make_blobs_f64")
+
+
+def rechecked(ws):
+    so = _lib.lib()
+    out = ctypes.c_int64(0)
+    _lib.check(so.dkm_screen_stats(ws.p, ctypes.byref(out), stream_ptr()),
+               "dkm_screen_stats")
+    return int(out.value)

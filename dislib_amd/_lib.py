@@ -1,0 +1,93 @@
+"""ctypes binding of ``libdkm.so`` (the C ABI declared in ``include/dkm.h``).
+
+The product path has no CPU fallback: if the HIP library is missing or no
+GPU is visible, :func:`lib` raises.  Symbols are resolved eagerly so that a
+stale or partial build fails at load time, not mid-fit.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DKM_LIB", os.path.join(_HERE, "libdkm.so"))
+
+# constants mirrored from include/dkm.h
+ABI_VERSION = 1
+MODE_AUTO, MODE_EXACT, MODE_SCREEN32 = 0, 1, 2
+SUMS_F64, SUMS_F32, SUMS_RECIP = 0, 1, 2
+PREP_CSR = 1
+
+_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_sz = ctypes.c_size_t
+_f64 = ctypes.c_double
+_u64 = ctypes.c_uint64
+
+# name -> (restype, argtypes): every entry point of include/dkm.h
+SIGNATURES = {
+    "dkm_abi_version": (_i32, []),
+    "dkm_last_error": (ctypes.c_char_p, []),
+    "dkm_workspace_bytes": (_sz, [_i64, _i64, _i64]),
+    "dkm_prepare_centers": (_i32, [_p, _i64, _i64, _i32, _p, _sz, _p, _p]),
+    "dkm_partial_sum_f64": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz,
+                                   _p, _p, _i32, _p]),
+    "dkm_partial_sum_f32": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz,
+                                   _p, _p, _i32, _p]),
+    "dkm_predict_f64": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz, _p,
+                               _i32, _p]),
+    "dkm_predict_f32": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz, _p,
+                               _i32, _p]),
+    "dkm_update_centers": (_i32, [_p, _p, _i64, _i64, _i32, _f64, _p, _p,
+                                  _p]),
+    "dkm_partial_sum_csr_f64": (_i32, [_p, _p, _p, _i64, _i64, _p, _i64, _p,
+                                       _sz, _p, _p, _p]),
+    "dkm_predict_csr_f64": (_i32, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _sz,
+                                   _p, _p]),
+    "dkm_make_blobs_f64": (_i32, [_p, _i64, _i64, _i64, _i64, _u64, _f64,
+                                  _f64, _p, _p]),
+    "dkm_screen_stats": (_i32, [_p, ctypes.POINTER(_i64), _p]),
+}
+
+_LIB = None
+
+
+class DkmError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load the shared library and bind every symbol (no GPU needed)."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise DkmError(
+            "libdkm.so not found at %s: build it with "
+            "`make -C dislib_amd/csrc` (or __graft_entry__.build())" % p)
+    so = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(so, name)           # AttributeError if not exported
+        fn.restype = res
+        fn.argtypes = args
+    if so.dkm_abi_version() != ABI_VERSION:
+        raise DkmError("libdkm ABI %d != %d" % (so.dkm_abi_version(),
+                                                 ABI_VERSION))
+    if path is None:
+        _LIB = so
+    return so
+
+
+def lib():
+    """The library for compute calls: requires a visible ROCm GPU."""
+    import torch
+    if not torch.cuda.is_available():
+        raise DkmError("dislib_amd needs an MI355X (ROCm) GPU: "
+                       "torch.cuda.is_available() is False")
+    return load()
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = _LIB.dkm_last_error().decode() if _LIB is not None else ""
+        raise DkmError("%s failed (code %d): %s" % (what, rc, msg))

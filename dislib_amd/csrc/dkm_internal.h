@@ -1,0 +1,213 @@
+// dkm_internal.h -- shared device helpers for libdkm (gfx950 / CDNA4 only).
+//
+// Compiled with -ffp-contract=off: the exact-arithmetic paths below must
+// round every product and sum separately, exactly like numpy on the host.
+// Where a fused multiply-add is wanted it is written explicitly (fma/fmaf).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/dkm.h"
+
+namespace dkm {
+
+constexpr int WAVE = 64;
+
+// ---------------------------------------------------------------------------
+// Error plumbing: a thread-local message, int return codes, no exceptions.
+// ---------------------------------------------------------------------------
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+int check_launch(const char *what);
+
+// ---------------------------------------------------------------------------
+// Workspace layout (caller-allocated device memory, carved here).
+// ---------------------------------------------------------------------------
+struct WsHeader {
+  uint64_t magic;
+  int64_t k, d, dpad, n_queue;
+  uint64_t cmax_bits;       // max_c ||c||_2 as ordered bits (non-negative)
+  uint32_t qcount;          // samples queued for exact re-check this call
+  uint32_t pad0;
+  uint64_t rechecked_total; // diagnostics
+  uint64_t reserved[8];
+};
+constexpr uint64_t WS_MAGIC = 0x444b4d5753303031ull;  // "DKMWS001"
+constexpr size_t WS_HDR = 256;
+
+__host__ __device__ inline int64_t round_up(int64_t a, int64_t b) {
+  return (a + b - 1) / b * b;
+}
+
+struct WsView {
+  WsHeader *hdr;
+  float *c32;     // k x dpad fp32 centres (zero padded)
+  float *cn32;    // k fp32 ||c||^2 (computed in fp64, rounded once)
+  double *cn64;   // k fp64 ||c||^2, sequential over t (sklearn row_norms)
+  double *ct64;   // d x k transposed centres (DKM_PREP_CSR)
+  int32_t *queue; // n_queue sample indices for the exact re-check
+};
+
+size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue);
+int64_t default_queue(int64_t k, int64_t d);
+int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v);
+
+// ---------------------------------------------------------------------------
+// numpy add.reduce order (loops_utils.h pairwise sum, 8192-element buffers).
+// `F` returns the t-th term.  Used on the exact paths only.
+// ---------------------------------------------------------------------------
+template <class F>
+__device__ __forceinline__ double pw_leaf(const F &f, int64_t lo, int64_t n) {
+  if (n < 8) {
+    double r = -0.0;
+    for (int64_t i = 0; i < n; ++i) r = r + f(lo + i);
+    return r;
+  }
+  double r0 = f(lo + 0), r1 = f(lo + 1), r2 = f(lo + 2), r3 = f(lo + 3);
+  double r4 = f(lo + 4), r5 = f(lo + 5), r6 = f(lo + 6), r7 = f(lo + 7);
+  const int64_t stop = n - (n & 7);
+  int64_t i = 8;
+  for (; i < stop; i += 8) {
+    r0 = r0 + f(lo + i + 0);
+    r1 = r1 + f(lo + i + 1);
+    r2 = r2 + f(lo + i + 2);
+    r3 = r3 + f(lo + i + 3);
+    r4 = r4 + f(lo + i + 4);
+    r5 = r5 + f(lo + i + 5);
+    r6 = r6 + f(lo + i + 6);
+    r7 = r7 + f(lo + i + 7);
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res = res + f(lo + i);
+  return res;
+}
+
+// Recursive halving above 128 elements, as an explicit post-order walk.
+template <class F>
+__device__ double pw_block(const F &f, int64_t lo, int64_t n) {
+  if (n <= 128) return pw_leaf(f, lo, n);
+  int64_t flo[16], fn[16];
+  double fleft[16];
+  int fstate[16];
+  int sp = 0;
+  flo[0] = lo;
+  fn[0] = n;
+  double val = 0.0;
+  bool have = false;
+  for (;;) {
+    if (!have) {
+      if (fn[sp] <= 128) {
+        val = pw_leaf(f, flo[sp], fn[sp]);
+        have = true;
+      } else {
+        int64_t n2 = fn[sp] / 2;
+        n2 -= n2 % 8;
+        fstate[sp] = 0;
+        flo[sp + 1] = flo[sp];
+        fn[sp + 1] = n2;
+        ++sp;
+        continue;
+      }
+    }
+    if (sp == 0) return val;
+    --sp;
+    int64_t n2 = fn[sp] / 2;
+    n2 -= n2 % 8;
+    if (fstate[sp] == 0) {
+      fleft[sp] = val;
+      fstate[sp] = 1;
+      flo[sp + 1] = flo[sp] + n2;
+      fn[sp + 1] = fn[sp] - n2;
+      ++sp;
+      have = false;
+    } else {
+      val = fleft[sp] + val;
+    }
+  }
+}
+
+template <class F>
+__device__ double pw_sum(const F &f, int64_t n) {
+  double res = 0.0;
+  for (int64_t s = 0; s < n; s += 8192) {
+    const int64_t m = (n - s) < 8192 ? (n - s) : 8192;
+    res = res + pw_block(f, s, m);
+  }
+  return res;
+}
+
+// Squared-difference term (x_t - c_t)^2, rounded exactly like numpy:
+// the difference, then the product, each correctly rounded (no FMA).
+template <class TX>
+struct SqDiff {
+  const TX *x;
+  const double *c;
+  __device__ __forceinline__ double operator()(int64_t t) const {
+    const double df = (double)x[t] - c[t];
+    return df * df;
+  }
+};
+
+// Register-resident exact distance for d <= MAXD (MAXD multiple of 8):
+// numpy's pairwise order specialised to n <= 128.  c may point to LDS.
+template <int MAXD, class CPTR>
+__device__ __forceinline__ double exact_sqdist_reg(const double (&x)[MAXD],
+                                                   CPTR c, int d) {
+  static_assert(MAXD % 8 == 0 && MAXD <= 128, "MAXD");
+  if (d < 8) {
+    double r = -0.0;
+#pragma unroll
+    for (int t = 0; t < 8 && t < MAXD; ++t)
+      if (t < d) {
+        const double df = x[t] - c[t];
+        r = r + df * df;
+      }
+    return r;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const double df = x[j] - c[j];
+    r[j] = df * df;
+  }
+  const int full = d - (d & 7);
+#pragma unroll
+  for (int b = 1; b < MAXD / 8; ++b) {
+    if (8 * b < full) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const double df = x[8 * b + j] - c[8 * b + j];
+        r[j] = r[j] + df * df;
+      }
+    }
+  }
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+  for (int t = 8; t < MAXD; ++t)
+    if (t >= full && t < d) {
+      const double df = x[t] - c[t];
+      res = res + df * df;
+    }
+  return res;
+}
+
+// (dist, idx) lexicographic minimum across a wave: first index wins ties.
+__device__ __forceinline__ void wave_argmin(double &dist, int &idx) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double od = __shfl_xor(dist, off, WAVE);
+    const int oi = __shfl_xor(idx, off, WAVE);
+    if (od < dist || (od == dist && oi < idx)) {
+      dist = od;
+      idx = oi;
+    }
+  }
+}
+
+__device__ __forceinline__ void atomic_add_f64(double *p, double v) {
+  unsafeAtomicAdd(p, v);  // global_atomic_add_f64 (no CAS loop on gfx950)
+}
+
+}  // namespace dkm

@@ -1,0 +1,119 @@
+// dkm_sparse.hip -- CSR Subset path.
+//
+// Replaces the sparse branch of `_partial_sum` / `_predict`
+// (cluster/kmeans/base.py:169,196), where the reference calls
+// sklearn.metrics.pairwise_distances(sample_csr, centres_csr) per sample.
+// sklearn 1.7.2 `_euclidean_distances` (metrics/pairwise.py:391-442) for
+// fp64 CSR inputs computes, per centre j,
+//   dot_j = scipy csr_matmat: sequential over the sample's stored entries,
+//           sums[j] += x_v * C[j][col_v]   (product then add, no FMA)
+//   xx    = sequential sum of x_v^2 over stored entries
+//   yy_j  = sequential sum of C[j][t]^2 over t (stored entries; exact zeros
+//           add nothing)
+//   dist_j = sqrt(max(0, ((-2 * dot_j) + xx) + yy_j))
+// followed by np.argmin (first index).  This kernel reproduces that
+// arithmetic bit-for-bit.
+//
+// Layout: one wave per sample, lanes over centres j = lane, lane+64, ...;
+// the centres are read transposed (C^T, d x k, built by dkm_prepare_centers
+// with DKM_PREP_CSR) so that the 64 lanes of a stored column read 512
+// contiguous bytes.  Sums are added with fp64 atomics (lanes over the
+// sample's stored entries).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+
+#include "dkm_internal.h"
+
+namespace dkm {
+
+__global__ void __launch_bounds__(256)
+    k_csr_assign(const int64_t *__restrict__ indptr,
+                 const int32_t *__restrict__ indices,
+                 const double *__restrict__ data, int64_t n, int d,
+                 const double *__restrict__ CT, const double *__restrict__ yy,
+                 int k, int32_t *labels, double *acc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave; i < n; i += nwaves) {
+    const int64_t a = indptr[i], b = indptr[i + 1];
+    double xx = 0.0;  // identical in every lane (broadcast loads)
+    for (int64_t v = a; v < b; ++v) xx = xx + data[v] * data[v];
+    double best = INFINITY;
+    int bi = 0x7fffffff;
+    for (int j = lane; j < k; j += 64) {
+      double dot = 0.0;
+      for (int64_t v = a; v < b; ++v)
+        dot = dot + data[v] * CT[(int64_t)indices[v] * k + j];
+      double dd = -2.0 * dot;
+      dd = dd + xx;
+      dd = dd + yy[j];
+      const double dist = sqrt(dd > 0.0 ? dd : 0.0);
+      if (dist < best || bi == 0x7fffffff) {
+        best = dist;
+        bi = j;
+      }
+    }
+    wave_argmin(best, bi);
+    if (lane == 0 && labels) labels[i] = bi;
+    if (acc) {
+      for (int64_t v = a + lane; v < b; v += 64)
+        atomic_add_f64(acc + (int64_t)bi * d + indices[v], data[v]);
+      if (lane == 0) atomic_add_f64(acc + (int64_t)k * d + bi, 1.0);
+    }
+  }
+}
+
+static int csr_assign(const int64_t *indptr, const int32_t *indices,
+                      const double *data, int64_t n, int64_t d,
+                      const double *C, int64_t k, const void *ws, size_t wsb,
+                      int32_t *labels, double *acc, void *stream,
+                      const char *who) {
+  if (n < 0 || d <= 0 || k <= 0 || d > INT32_MAX || k > INT32_MAX)
+    return fail(DKM_E_ARG, std::string(who) + ": bad n/d/k");
+  if (n == 0) return 0;
+  if (!indptr || !C || (!indices && !data))
+    return fail(DKM_E_ARG, std::string(who) + ": NULL input");
+  (void)C;  // the kernel reads C^T and |c|^2 prepared in the workspace
+  WsView v;
+  if (int r = ws_view(ws, wsb, k, d, &v)) return r;
+  int dev = 0, cus = 256;
+  hipDeviceProp_t p;
+  if (hipGetDevice(&dev) == hipSuccess &&
+      hipGetDeviceProperties(&p, dev) == hipSuccess)
+    cus = p.multiProcessorCount;
+  const int64_t blocks = std::min<int64_t>((n + 3) / 4, (int64_t)cus * 16);
+  k_csr_assign<<<(unsigned)std::max<int64_t>(1, blocks), 256, 0,
+                 (hipStream_t)stream>>>(indptr, indices, data, n, (int)d,
+                                        v.ct64, v.cn64, (int)k, labels, acc);
+  return check_launch(who);
+}
+
+}  // namespace dkm
+
+using namespace dkm;
+
+extern "C" {
+
+int dkm_partial_sum_csr_f64(const int64_t *indptr, const int32_t *indices,
+                            const double *data, int64_t n, int64_t d,
+                            const double *C, int64_t k, const void *ws,
+                            size_t ws_bytes, int32_t *labels, double *acc,
+                            void *stream) {
+  if (!acc) return fail(DKM_E_ARG, "partial_sum_csr: acc is NULL");
+  return csr_assign(indptr, indices, data, n, d, C, k, ws, ws_bytes, labels,
+                    acc, stream, "dkm_partial_sum_csr_f64");
+}
+
+int dkm_predict_csr_f64(const int64_t *indptr, const int32_t *indices,
+                        const double *data, int64_t n, int64_t d,
+                        const double *C, int64_t k, const void *ws,
+                        size_t ws_bytes, int32_t *labels, void *stream) {
+  if (!labels) return fail(DKM_E_ARG, "predict_csr: labels is NULL");
+  return csr_assign(indptr, indices, data, n, d, C, k, ws, ws_bytes, labels,
+                    nullptr, stream, "dkm_predict_csr_f64");
+}
+
+}  // extern "C"

@@ -1,0 +1,295 @@
+// dkm_util.hip -- error plumbing, workspace, centre preparation, centre
+// update + convergence criterion, synthetic blob generator.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "dkm_internal.h"
+
+namespace dkm {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string &msg) { g_err = msg; }
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+int check_launch(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return fail((int)e, std::string(what) + ": " + hipGetErrorString(e));
+  return 0;
+}
+
+int64_t default_queue(int64_t k, int64_t d) {
+  (void)k;
+  (void)d;
+  return int64_t(1) << 22;  // 4M re-check slots (16 MB); overflow -> inline
+}
+
+size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
+  if (n_queue <= 0) n_queue = default_queue(k, d);
+  const int64_t dpad = round_up(d, 4);
+  size_t b = WS_HDR;
+  b += round_up(k * dpad * 4, 256);   // c32
+  b += round_up(k * 4, 256);          // cn32
+  b += round_up(k * 8, 256);          // cn64
+  b += round_up(k * d * 8, 256);      // ct64
+  b += round_up(n_queue * 4, 256);    // queue
+  return b;
+}
+
+int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
+  if (!ws) return fail(DKM_E_ARG, "workspace is NULL");
+  const int64_t dpad = round_up(d, 4);
+  char *p = (char *)ws;
+  v->hdr = (WsHeader *)p;
+  p += WS_HDR;
+  v->c32 = (float *)p;
+  p += round_up(k * dpad * 4, 256);
+  v->cn32 = (float *)p;
+  p += round_up(k * 4, 256);
+  v->cn64 = (double *)p;
+  p += round_up(k * 8, 256);
+  v->ct64 = (double *)p;
+  p += round_up(k * d * 8, 256);
+  v->queue = (int32_t *)p;
+  const size_t fixed = (size_t)(p - (char *)ws);
+  if (bytes < fixed + 256)
+    return fail(DKM_E_WORKSPACE, "workspace too small for k/d");
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// prepare: header + fp32 centres + norms + cmax
+// ---------------------------------------------------------------------------
+__global__ void k_ws_header(WsHeader *h, int64_t k, int64_t d, int64_t dpad,
+                            int64_t n_queue) {
+  if (threadIdx.x == 0) {
+    h->magic = WS_MAGIC;
+    h->k = k;
+    h->d = d;
+    h->dpad = dpad;
+    h->n_queue = n_queue;
+    h->cmax_bits = 0;
+    h->qcount = 0;  // rechecked_total accumulates over the workspace life
+  }
+}
+
+// one 256-thread block per centre
+__global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ C,
+                                                 int64_t k, int64_t d,
+                                                 int64_t dpad, int flags,
+                                                 WsView v) {
+  const int64_t c = blockIdx.x;
+  const double *row = C + c * d;
+  for (int64_t t = threadIdx.x; t < dpad; t += blockDim.x) {
+    const double val = t < d ? row[t] : 0.0;
+    v.c32[c * dpad + t] = (float)val;
+    if ((flags & DKM_PREP_CSR) && t < d) v.ct64[t * k + c] = val;
+  }
+  if (threadIdx.x == 0) {
+    // sequential over t: sklearn row_norms(squared=True) order
+    // (utils/sparsefuncs_fast.pyx:26-44); exact zeros change nothing.
+    double n2 = 0.0;
+    for (int64_t t = 0; t < d; ++t) n2 = n2 + row[t] * row[t];
+    v.cn64[c] = n2;
+    v.cn32[c] = (float)n2;
+    const double nrm = sqrt(n2);
+    // non-negative doubles order like their bit patterns
+    atomicMax((unsigned long long *)&v.hdr->cmax_bits,
+              (unsigned long long)__double_as_longlong(nrm));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// update: C[c] = sums/counts (counts != 0), per-centre shift, criterion
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_update(const double *__restrict__ acc,
+                                                double *__restrict__ C,
+                                                int64_t k, int64_t d, int mode,
+                                                double *__restrict__ shift) {
+  const int64_t c = blockIdx.x;
+  const double cnt = acc[k * d + c];
+  __shared__ double red[256];
+  double ss = 0.0;
+  if (mode == DKM_SUMS_RECIP) {
+    // sparse criterion (sklearn euclidean_distances, sequential sums):
+    // computed from old and new rows before the new row is stored.
+    if (threadIdx.x == 0) {
+      double dot = 0.0, aa = 0.0, bb = 0.0;
+      const double inv = cnt != 0.0 ? 1.0 / cnt : 0.0;
+      for (int64_t t = 0; t < d; ++t) {
+        const double old = C[c * d + t];
+        const double nv = cnt != 0.0 ? acc[c * d + t] * inv : old;
+        dot = dot + nv * old;
+        aa = aa + nv * nv;
+        bb = bb + old * old;
+      }
+      double dd = -2.0 * dot;
+      dd = dd + aa;
+      dd = dd + bb;
+      shift[1 + c] = sqrt(dd > 0.0 ? dd : 0.0);
+    }
+    __syncthreads();
+    if (cnt != 0.0) {
+      const double inv = 1.0 / cnt;
+      for (int64_t t = threadIdx.x; t < d; t += blockDim.x)
+        C[c * d + t] = acc[c * d + t] * inv;
+    }
+    return;
+  }
+  if (cnt != 0.0) {
+    for (int64_t t = threadIdx.x; t < d; t += blockDim.x) {
+      const double s = acc[c * d + t];
+      double nv;
+      if (mode == DKM_SUMS_F32)
+        nv = (double)((float)s / (float)cnt);
+      else
+        nv = s / cnt;
+      const double old = C[c * d + t];
+      const double df = nv - old;
+      ss = fma(df, df, ss);
+      C[c * d + t] = nv;
+    }
+  }
+  red[threadIdx.x] = ss;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) shift[1 + c] = sqrt(red[0]);
+}
+
+// sequential sum over centres in index order (base.py:128-129), one lane
+__global__ void k_criterion(double *shift, int64_t k, double tol2,
+                            int32_t *flag) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    double diff = 0.0;
+    for (int64_t c = 0; c < k; ++c) diff = diff + shift[1 + c];
+    shift[0] = diff;
+    if (flag) *flag = (diff < tol2) ? 1 : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic make_blobs (counter-based; mirrors oracle.make_blobs_rows)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) k_blobs(double *__restrict__ X,
+                                               int64_t row0, int64_t n,
+                                               int64_t d, int64_t n_blobs,
+                                               uint64_t seed, double box,
+                                               double stdv,
+                                               int32_t *__restrict__ blob) {
+  const uint64_t sm = seed << 40;
+  const int64_t total = n * d;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / d, t = e - (e / d) * d;
+    const uint64_t row = (uint64_t)(row0 + i);
+    const uint64_t b = splitmix64(row ^ sm ^ 0xB10Bull) % (uint64_t)n_blobs;
+    const uint64_t cc = (b * (uint64_t)d + (uint64_t)t) + seed * 0x100000000ull;
+    const double u0 = (double)(splitmix64(cc ^ 0xC0FFEEull) >> 11) * 0x1.0p-53;
+    const double cen = (2.0 * u0 - 1.0) * box;
+    const uint64_t ctr = (row * (uint64_t)d + (uint64_t)t) ^ sm;
+    const uint64_t h1 = splitmix64(ctr * 2ull);
+    const uint64_t h2 = splitmix64(ctr * 2ull + 1ull);
+    const double u1 = ((double)(h1 >> 11) + 1.0) * 0x1.0p-53;
+    const double u2 = (double)(h2 >> 11) * 0x1.0p-53;
+    const double z = sqrt(-2.0 * log(u1)) * cos(2.0 * M_PI * u2);
+    X[i * d + t] = cen + stdv * z;
+    if (blob && t == 0) blob[i] = (int32_t)b;
+  }
+}
+
+}  // namespace dkm
+
+using namespace dkm;
+
+extern "C" {
+
+int dkm_abi_version(void) { return DKM_ABI_VERSION; }
+
+const char *dkm_last_error(void) { return g_err.c_str(); }
+
+size_t dkm_workspace_bytes(int64_t k, int64_t d, int64_t n_queue) {
+  if (k <= 0 || d <= 0) return 0;
+  return ws_bytes(k, d, n_queue);
+}
+
+int dkm_prepare_centers(const double *C, int64_t k, int64_t d, int flags,
+                        void *ws, size_t ws_b, double *acc, void *stream) {
+  if (!C || k <= 0 || d <= 0) return fail(DKM_E_ARG, "prepare: bad C/k/d");
+  if (k > INT32_MAX) return fail(DKM_E_ARG, "prepare: k too large");
+  WsView v;
+  if (int r = ws_view(ws, ws_b, k, d, &v)) return r;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t dpad = round_up(d, 4);
+  const size_t fixed = (size_t)((char *)v.queue - (char *)ws);
+  const int64_t nq = (int64_t)((ws_b - fixed) / 4);
+  k_ws_header<<<1, 64, 0, s>>>(v.hdr, k, d, dpad, nq);
+  k_prepare<<<(unsigned)k, 256, 0, s>>>(C, k, d, dpad, flags, v);
+  if (int r = check_launch("dkm_prepare_centers")) return r;
+  if (acc) {
+    hipError_t e = hipMemsetAsync(acc, 0, (size_t)(k * (d + 1)) * 8, s);
+    if (e != hipSuccess)
+      return fail((int)e, std::string("prepare: memset acc: ") +
+                              hipGetErrorString(e));
+  }
+  return 0;
+}
+
+int dkm_update_centers(const double *acc, double *C, int64_t k, int64_t d,
+                       int sums_mode, double tol, double *diff, int32_t *flag,
+                       void *stream) {
+  if (!acc || !C || !diff || k <= 0 || d <= 0)
+    return fail(DKM_E_ARG, "update: bad arguments");
+  if (sums_mode < DKM_SUMS_F64 || sums_mode > DKM_SUMS_RECIP)
+    return fail(DKM_E_ARG, "update: bad sums_mode");
+  hipStream_t s = (hipStream_t)stream;
+  k_update<<<(unsigned)k, 256, 0, s>>>(acc, C, k, d, sums_mode, diff);
+  k_criterion<<<1, 64, 0, s>>>(diff, k, tol * tol, flag);
+  return check_launch("dkm_update_centers");
+}
+
+int dkm_make_blobs_f64(double *X, int64_t row0, int64_t n, int64_t d,
+                       int64_t n_blobs, uint64_t seed, double box, double std,
+                       int32_t *blob, void *stream) {
+  if (!X || n < 0 || d <= 0 || n_blobs <= 0 || row0 < 0)
+    return fail(DKM_E_ARG, "make_blobs: bad arguments");
+  if (n == 0) return 0;
+  const int64_t total = n * d;
+  int64_t grid = (total + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  k_blobs<<<(unsigned)grid, 256, 0, (hipStream_t)stream>>>(
+      X, row0, n, d, n_blobs, seed, box, std, blob);
+  return check_launch("dkm_make_blobs_f64");
+}
+
+int dkm_screen_stats(const void *ws, int64_t *n_rechecked, void *stream) {
+  if (!ws || !n_rechecked) return fail(DKM_E_ARG, "screen_stats: NULL");
+  WsHeader h;
+  hipError_t e = hipMemcpyAsync(&h, ws, sizeof(h), hipMemcpyDeviceToHost,
+                                (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  if (e != hipSuccess)
+    return fail((int)e, std::string("screen_stats: ") + hipGetErrorString(e));
+  if (h.magic != WS_MAGIC) return fail(DKM_E_ARG, "screen_stats: bad ws");
+  *n_rechecked = (int64_t)h.rechecked_total;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,138 @@
+/*
+ * dkm.h -- C ABI of libdkm.so, the MI355X (gfx950) k-means Lloyd hot path.
+ *
+ * Drop-in boundary for dislib's k-means (reference: /root/reference,
+ * dislib v0.2.0).  The reference is pure Python over PyCOMPSs tasks; the
+ * functions below replace its per-Subset task bodies and its reduction tree.
+ * Each entry cites the reference function it replaces.
+ *
+ * Conventions
+ *  - All array pointers are DEVICE pointers (hipMalloc / torch CUDA tensors)
+ *    unless documented otherwise.  The caller owns every buffer; the library
+ *    never allocates or frees caller memory.  A scratch area ("workspace") of
+ *    dkm_workspace_bytes() bytes is provided by the caller.
+ *  - Every call is asynchronous and stream-ordered on `stream` (a
+ *    hipStream_t passed as void*; NULL = the legacy default stream).
+ *  - Every call returns 0 on success, or a nonzero DKM_E_* / hipError_t code;
+ *    dkm_last_error() returns a thread-local message for the last failure.
+ *    No C++ exception ever crosses this boundary.
+ *  - Matrices are row-major with a leading dimension (elements) `ld`.
+ */
+#ifndef DKM_H
+#define DKM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DKM_ABI_VERSION 1
+
+/* error codes (besides hipError_t values passed through) */
+#define DKM_OK 0
+#define DKM_E_ARG 10001       /* invalid argument / shape                    */
+#define DKM_E_WORKSPACE 10002 /* workspace too small                         */
+#define DKM_E_LAUNCH 10003    /* kernel launch failed                        */
+
+/* assignment modes (flags) */
+#define DKM_MODE_AUTO 0     /* library picks: SCREEN32 when profitable       */
+#define DKM_MODE_EXACT 1    /* direct ||x-c||^2 in numpy's pairwise order for
+                               every (sample, centre): reference arithmetic   */
+#define DKM_MODE_SCREEN32 2 /* fp32 ||c||^2-2x.c screen with a rigorous error
+                               bound; ambiguous samples re-checked with the
+                               EXACT arithmetic.  Labels identical to EXACT. */
+
+/* sum-dtype flags for dkm_update_centers (reference keeps X's dtype for the
+ * partial sums; base.py:178 and :147) */
+#define DKM_SUMS_F64 0
+#define DKM_SUMS_F32 1  /* fp32 samples: centre = fl32(fl32(sum)/fl32(count)) */
+#define DKM_SUMS_RECIP 2 /* sparse: centre = sum * (1.0/count) (scipy divide) */
+
+int dkm_abi_version(void);
+const char *dkm_last_error(void);
+
+/* Workspace needed for k centres of d features and up to n_queue re-check
+ * slots (n_queue = 0 lets the library pick).  Host function. */
+size_t dkm_workspace_bytes(int64_t k, int64_t d, int64_t n_queue);
+
+/* prepare flags */
+#define DKM_PREP_CSR 1 /* also build the transposed fp64 centres C^T (d x k)
+                          used by the CSR kernels                           */
+
+/* Derive per-iteration centre data (fp32 copy, |c|^2 in sklearn's sequential
+ * order, error-bound scalars, optionally C^T) into the workspace and ZERO the
+ * accumulator acc[k*(d+1)] ([sums | counts]) when acc != NULL.  Replaces the
+ * implicit per-task centre broadcast of base.py:110,114 (and sklearn's
+ * row_norms of the centres, recomputed per sample by the reference).      */
+int dkm_prepare_centers(const double *C, int64_t k, int64_t d, int flags,
+                        void *ws, size_t ws_bytes, double *acc, void *stream);
+
+/* Fused assignment + per-cluster sum/count for dense samples.
+ * Replaces `_partial_sum` (cluster/kmeans/base.py:166-181), including
+ * `_vec_matrix_euclid` (:204-205), `np.argmin` (:173) and `set_label` (:176).
+ * Accumulates into acc = [sums k*d | counts k] (fp64, += semantics; call
+ * dkm_prepare_centers first in an iteration).  labels (int32[n]) may be NULL
+ * when not wanted.  X is fp64 (…_f64) or fp32 (…_f32); C is always fp64.  */
+int dkm_partial_sum_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
+                        const double *C, int64_t k, const void *ws,
+                        size_t ws_bytes, int32_t *labels, double *acc,
+                        int mode, void *stream);
+int dkm_partial_sum_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
+                        const double *C, int64_t k, const void *ws,
+                        size_t ws_bytes, int32_t *labels, double *acc,
+                        int mode, void *stream);
+
+/* Assignment only.  Replaces `_predict` (base.py:194-201).  Needs a prepared
+ * workspace (dkm_prepare_centers with acc = NULL is allowed).             */
+int dkm_predict_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
+                    const double *C, int64_t k, const void *ws,
+                    size_t ws_bytes, int32_t *labels, int mode, void *stream);
+int dkm_predict_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
+                    const double *C, int64_t k, const void *ws,
+                    size_t ws_bytes, int32_t *labels, int mode, void *stream);
+
+/* Centre recomputation + convergence criterion.  Replaces
+ * `_recompute_centers` (base.py:137-147, the division and empty-cluster
+ * rule) and the criterion of `_converged` (:122-135):
+ *   C[c] = sums[c] / counts[c] for counts[c] != 0 (else unchanged),
+ *   diff[1+c] = ||C_new[c] - C_old[c]||_2, diff[0] = sum over c in index
+ *   order (diff: device buffer of k+1 doubles), and
+ *   *flag = (diff[0] < tol*tol) ? 1 : 0 (flag nullable).
+ * For DKM_SUMS_RECIP (sparse input) the per-centre distance follows
+ * sklearn's sqrt(max(0, (-2 a.b + |a|^2) + |b|^2)) with sequential sums, as
+ * the reference's sparse criterion does (base.py:123 pairwise_distances).
+ * acc is the (all-reduced) [sums | counts] buffer.  sums_mode: DKM_SUMS_*. */
+int dkm_update_centers(const double *acc, double *C, int64_t k, int64_t d,
+                       int sums_mode, double tol, double *diff,
+                       int32_t *flag, void *stream);
+
+/* CSR samples (int64 indptr[n+1], int32 indices, fp64 data; d columns).
+ * Replaces the sparse branch of `_partial_sum`/`_predict` (base.py:169,196:
+ * sklearn euclidean_distances = sqrt(max(0, (-2 x.c + |x|^2) + |c|^2))).  */
+int dkm_partial_sum_csr_f64(const int64_t *indptr, const int32_t *indices,
+                            const double *data, int64_t n, int64_t d,
+                            const double *C, int64_t k, const void *ws,
+                            size_t ws_bytes, int32_t *labels, double *acc,
+                            void *stream);
+int dkm_predict_csr_f64(const int64_t *indptr, const int32_t *indices,
+                        const double *data, int64_t n, int64_t d,
+                        const double *C, int64_t k, const void *ws,
+                        size_t ws_bytes, int32_t *labels, void *stream);
+
+/* Synthetic make_blobs rows [row0, row0+n) into X (n x d, ld = d), blob ids
+ * into blob (nullable).  Counter-based: any row range regenerates
+ * identically.  Bench/test data generator, not part of the reference path. */
+int dkm_make_blobs_f64(double *X, int64_t row0, int64_t n, int64_t d,
+                       int64_t n_blobs, uint64_t seed, double box, double std,
+                       int32_t *blob, void *stream);
+
+/* Diagnostics of the last SCREEN32 call on this workspace (device -> host,
+ * synchronous on `stream`): number of samples sent to the exact re-check.  */
+int dkm_screen_stats(const void *ws, int64_t *n_rechecked, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DKM_H */
