@@ -23,7 +23,8 @@ accumulated in a different order than the reference's sequential
 Subset-then-arity-tree order, so centres agree to ~1e-15 relative instead of
 bit-for-bit; ``arity`` is kept but has no effect on the GPU (no reduction
 tree).  Extra keyword-only arguments select the assignment arithmetic
-(``mode``: "auto" | "exact" | "screen32", identical labels) and the device.
+(``mode``: "auto" | "exact" | "screen32" | "bf16x3", identical labels) and
+the device.
 """
 import numpy as np
 from scipy.sparse import csr_matrix, issparse
@@ -31,7 +32,7 @@ from scipy.sparse import csr_matrix, issparse
 from .. import _lib, _shard
 
 _MODES = {"auto": _lib.MODE_AUTO, "exact": _lib.MODE_EXACT,
-          "screen32": _lib.MODE_SCREEN32}
+          "screen32": _lib.MODE_SCREEN32, "bf16x3": _lib.MODE_BF16X3}
 
 
 def _init_centers(n_features, sparse, n_clusters, random_state):
@@ -154,7 +155,7 @@ class _Lloyd:
                               ).to(dd.device)
         if broadcast_init:
             _shard.broadcast_(self.C)     # ranks must start identically
-        self.ws = Workspace(k, d, max(1, min(dd.n, 1 << 24)), dd.device)
+        self.ws = Workspace(k, d, max(1, min(dd.n, 1 << 27)), dd.device)
         self.acc = t.empty(k * (d + 1), dtype=t.float64, device=dd.device)
         self.diff = t.zeros(k + 1, dtype=t.float64, device=dd.device)
         self.flag = t.zeros(1, dtype=t.int32, device=dd.device)

@@ -47,8 +47,16 @@ struct WsView {
   float *cn32;    // k fp32 ||c||^2 (computed in fp64, rounded once)
   double *cn64;   // k fp64 ||c||^2, sequential over t (sklearn row_norms)
   double *ct64;   // d x k transposed centres (DKM_PREP_CSR)
+  float *cfrag;   // fp32 centres in MFMA A-fragment order (see dkm_dense)
+  float *cnpad;   // kpad16 fp32 ||c||^2, +inf for padding centres
+  uint16_t *bfrag; // bf16 hi/lo centres in 16x16x32 MFMA fragment order
   int32_t *queue; // n_queue sample indices for the exact re-check
 };
+
+// MFMA fragment tiling of the centres: 16 centres x 16 dims per 1 KB block.
+__host__ __device__ inline int64_t kpad16(int64_t k) { return (k + 15) / 16 * 16; }
+__host__ __device__ inline int64_t dpad16(int64_t d) { return (d + 15) / 16 * 16; }
+__host__ __device__ inline int64_t dpad32(int64_t d) { return (d + 31) / 32 * 32; }
 
 size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue);
 int64_t default_queue(int64_t k, int64_t d);

@@ -43,6 +43,9 @@ extern "C" {
 #define DKM_MODE_SCREEN32 2 /* fp32 ||c||^2-2x.c screen with a rigorous error
                                bound; ambiguous samples re-checked with the
                                EXACT arithmetic.  Labels identical to EXACT. */
+#define DKM_MODE_SCREEN_BF16X3 3 /* same, x.c from bf16 hi/lo splits on the
+                               bf16 MFMA (hi*hi + hi*lo + lo*hi); its own
+                               bound; labels identical to EXACT.            */
 
 /* sum-dtype flags for dkm_update_centers (reference keeps X's dtype for the
  * partial sums; base.py:178 and :147) */

@@ -17,6 +17,8 @@ step() {  # name limit cmd...
 }
 step pytest 900 python -m pytest tests -m gpu -q -p no:cacheprovider --maxfail=10 "$@"
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step modes 300 python tools/bench_modes.py --rounds 5 --modes screen32,bf16x3
+step modes_init 300 python tools/bench_modes.py --rounds 3 --modes screen32,bf16x3 --centres init
 step bench 400 python bench.py --steps 20 --warmup 3
 step prof 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/${TAG}_prof -o run -- python bench.py --steps 10 --warmup 2 --no-cpu
 echo "== done"
