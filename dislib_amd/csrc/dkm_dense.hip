@@ -59,17 +59,29 @@ __device__ __forceinline__ double ld_x(const TX *p) {
   return (double)(*p);
 }
 
+// LDS accumulators: row stride of an odd number of doubles, so that the
+// rows of different clusters start in different banks (a 32-double row is
+// exactly one 256-B bank row: unpadded, every cluster's feature t sits in
+// the same bank and same-feature adds of different clusters serialise).
+__host__ __device__ __forceinline__ int lds_stride(int d) {
+  return (d & 1) ? d : d + 1;
+}
+__host__ __device__ __forceinline__ int64_t lds_acc_len(int64_t k, int d) {
+  return k * lds_stride(d) + k;
+}
+
 // Add a sample row to its cluster's sum (and count) -- lane-per-sample form.
 template <class TX>
 __device__ __forceinline__ void acc_row_lane(int amode, double *lds_acc,
                                              double *acc, int64_t k, int d,
                                              int label, const TX *xrow) {
   if (amode == ACC_LDS) {
-    double *srow = lds_acc + (int64_t)label * d;
+    const int ds = lds_stride(d);
+    double *srow = lds_acc + (int64_t)label * ds;
     for (int t = 0; t < d; ++t)
       __hip_atomic_fetch_add(srow + t, ld_x(xrow + t), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add(lds_acc + k * d + label, 1.0, __ATOMIC_RELAXED,
+    __hip_atomic_fetch_add(lds_acc + k * ds + label, 1.0, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
   } else if (amode == ACC_GLOBAL) {
     double *srow = acc + (int64_t)label * d;
@@ -78,10 +90,19 @@ __device__ __forceinline__ void acc_row_lane(int amode, double *lds_acc,
   }
 }
 
+__device__ __forceinline__ void zero_lds_acc(double *lds_acc, int64_t k,
+                                             int d) {
+  const int64_t len = lds_acc_len(k, d);
+  for (int64_t e = threadIdx.x; e < len; e += blockDim.x) lds_acc[e] = 0.0;
+}
+
 __device__ __forceinline__ void flush_lds_acc(const double *lds_acc,
-                                              double *acc, int64_t len) {
-  for (int64_t e = threadIdx.x; e < len; e += blockDim.x) {
-    const double v = lds_acc[e];
+                                              double *acc, int64_t k, int d) {
+  const int ds = lds_stride(d);
+  const int64_t kd = k * d;
+  for (int64_t e = threadIdx.x; e < kd + k; e += blockDim.x) {
+    const double v = e < kd ? lds_acc[(e / d) * ds + (e % d)]
+                            : lds_acc[k * ds + (e - kd)];
     if (v != 0.0) atomic_add_f64(acc + e, v);
   }
 }
@@ -99,9 +120,7 @@ __global__ void __launch_bounds__(BLOCK)
   double *lds_acc = smem + (int64_t)k * d;   // k*(d+1) accumulators
   const int64_t kd = (int64_t)k * d;
   for (int64_t e = threadIdx.x; e < kd; e += blockDim.x) cl[e] = C[e];
-  if (amode == ACC_LDS)
-    for (int64_t e = threadIdx.x; e < kd + k; e += blockDim.x)
-      lds_acc[e] = 0.0;
+  if (amode == ACC_LDS) zero_lds_acc(lds_acc, k, d);
   __syncthreads();
 
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -132,7 +151,7 @@ __global__ void __launch_bounds__(BLOCK)
   }
   if (amode == ACC_LDS) {
     __syncthreads();
-    flush_lds_acc(lds_acc, acc, kd + k);
+    flush_lds_acc(lds_acc, acc, k, d);
   }
 }
 
@@ -168,8 +187,7 @@ __global__ void __launch_bounds__(BLOCK)
   double *lds_acc = smem;
   const int64_t kd = (int64_t)k * d;
   if (amode == ACC_LDS) {
-    for (int64_t e = threadIdx.x; e < kd + k; e += blockDim.x)
-      lds_acc[e] = 0.0;
+    zero_lds_acc(lds_acc, k, d);
     __syncthreads();
   }
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -182,7 +200,7 @@ __global__ void __launch_bounds__(BLOCK)
   }
   if (amode == ACC_LDS) {
     __syncthreads();
-    flush_lds_acc(lds_acc, acc, kd + k);
+    flush_lds_acc(lds_acc, acc, k, d);
   }
 }
 
@@ -250,8 +268,7 @@ __global__ void __launch_bounds__(BLOCK)
     f32x4 *dst = (f32x4 *)cf;
     for (int e = threadIdx.x; e < nkb * NDB * 64; e += BLOCK) dst[e] = src[e];
     for (int e = threadIdx.x; e < nkb * 16; e += BLOCK) cn[e] = v.cnpad[e];
-    if (amode == ACC_LDS)
-      for (int64_t e = threadIdx.x; e < kd + k; e += BLOCK) lds_acc[e] = 0.0;
+    if (amode == ACC_LDS) zero_lds_acc(lds_acc, k, d);
   }
   const double cm = __longlong_as_double((long long)v.hdr->cmax_bits);
   const int64_t nq = v.hdr->n_queue;
@@ -338,7 +355,7 @@ __global__ void __launch_bounds__(BLOCK)
     }
     if (q == 0 && labels) labels[si] = i1;
     if (amode == ACC_LDS) {
-      double *srow = lds_acc + (int64_t)i1 * d;
+      double *srow = lds_acc + (int64_t)i1 * lds_stride(d);
 #pragma unroll
       for (int db = 0; db < NDB; ++db)
 #pragma unroll
@@ -349,8 +366,8 @@ __global__ void __launch_bounds__(BLOCK)
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       if (q == 0)
-        __hip_atomic_fetch_add(lds_acc + kd + i1, 1.0, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(lds_acc + (int64_t)k * lds_stride(d) + i1, 1.0,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else if (amode == ACC_GLOBAL) {
       double *srow = acc + (int64_t)i1 * d;
 #pragma unroll
@@ -365,7 +382,7 @@ __global__ void __launch_bounds__(BLOCK)
   }
   if (amode == ACC_LDS) {
     __syncthreads();
-    flush_lds_acc(lds_acc, acc, kd + k);
+    flush_lds_acc(lds_acc, acc, k, d);
   }
 }
 
@@ -438,8 +455,7 @@ __global__ void __launch_bounds__(SBLOCK)
     const bf16x8 *src = (const bf16x8 *)v.bfrag;
     for (int e = threadIdx.x; e < nkb * NKS * 128; e += SBLOCK) cf[e] = src[e];
     for (int e = threadIdx.x; e < nkb * 16; e += SBLOCK) cn[e] = v.cnpad[e];
-    if (amode == ACC_LDS)
-      for (int64_t e = threadIdx.x; e < kd + k; e += SBLOCK) lds_acc[e] = 0.0;
+    if (amode == ACC_LDS) zero_lds_acc(lds_acc, k, d);
   }
   const double cm = __longlong_as_double((long long)v.hdr->cmax_bits);
   const int64_t nq = v.hdr->n_queue;
@@ -549,7 +565,7 @@ __global__ void __launch_bounds__(SBLOCK)
       const int lab = i1[b];
       if (q == 0 && labels) labels[si] = lab;
       if (amode == ACC_LDS) {
-        double *srow = lds_acc + (int64_t)lab * d;
+        double *srow = lds_acc + (int64_t)lab * lds_stride(d);
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
@@ -560,7 +576,8 @@ __global__ void __launch_bounds__(SBLOCK)
                                      __HIP_MEMORY_SCOPE_WORKGROUP);
           }
         if (q == 0)
-          __hip_atomic_fetch_add(lds_acc + kd + lab, 1.0, __ATOMIC_RELAXED,
+          __hip_atomic_fetch_add(lds_acc + (int64_t)k * lds_stride(d) + lab,
+                                 1.0, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
       } else if (amode == ACC_GLOBAL) {
         double *srow = acc + (int64_t)lab * d;
@@ -577,7 +594,7 @@ __global__ void __launch_bounds__(SBLOCK)
   }
   if (amode == ACC_LDS) {
     __syncthreads();
-    flush_lds_acc(lds_acc, acc, kd + k);
+    flush_lds_acc(lds_acc, acc, k, d);
   }
 }
 
@@ -597,13 +614,14 @@ __global__ void __launch_bounds__(BLOCK)
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t qi = wave; qi < total; qi += nwaves) {
-    const int64_t i = base + v.queue[qi];
+    const int64_t i =
+        base + __builtin_amdgcn_readfirstlane(v.queue[qi]);  // wave-uniform
     const TX *xr = X + i * ldx;
     double best = INFINITY;
     int bi = 0x7fffffff;
     for (int jc = lane; jc < k; jc += 64) {
       const double dist =
-          sqrt(pw_leaf(SqDiff<TX>{xr, C + (int64_t)jc * d}, 0, d));
+          sqrt(pw_leaf(SqDiffT<TX>{xr, v.ct64 + jc, (int64_t)k}, 0, d));
       if (dist < best || bi == 0x7fffffff) {
         best = dist;
         bi = jc;
@@ -684,7 +702,7 @@ static int launch_exact(const TX *X, int64_t n, int d, int64_t ldx,
                         hipStream_t s) {
   const int64_t kd = (int64_t)k * d;
   const size_t c_bytes = (size_t)kd * 8;
-  const size_t a_bytes = (size_t)(kd + k) * 8;
+  const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
   const int maxd = pick_maxd(d);
   const bool creg = maxd > 0 && maxd <= 64 && c_bytes <= LDS_BUDGET;
   int amode = ACC_NONE;
@@ -740,7 +758,7 @@ static int launch_screen(const TX *X, int64_t n, int d, int64_t ldx,
                          int32_t *labels, double *acc, hipStream_t s) {
   const int64_t kd = (int64_t)k * d;
   const size_t cb = screen_lds_fixed(k, d);
-  const size_t a_bytes = (size_t)(kd + k) * 8;
+  const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
   int amode = ACC_NONE;
   if (acc) amode = (cb + a_bytes <= LDS_BUDGET) ? ACC_LDS : ACC_GLOBAL;
   const size_t lds = cb + (amode == ACC_LDS ? a_bytes : 0);
@@ -837,7 +855,7 @@ static int launch_screen_b3(const TX *X, int64_t n, int d, int64_t ldx,
                             hipStream_t s) {
   const int64_t kd = (int64_t)k * d;
   const size_t cb = b3_lds_fixed(k, d);
-  const size_t a_bytes = (size_t)(kd + k) * 8;
+  const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
   int amode = ACC_NONE;
   if (acc) amode = (cb + a_bytes <= LDS_BUDGET) ? ACC_LDS : ACC_GLOBAL;
   const size_t lds = cb + (amode == ACC_LDS ? a_bytes : 0);

@@ -158,6 +158,18 @@ struct SqDiff {
   }
 };
 
+// Same term against transposed centres C^T (d x k): lane-coalesced reads.
+template <class TX>
+struct SqDiffT {
+  const TX *x;
+  const double *ct;  // &C^T[0][j]
+  int64_t k;
+  __device__ __forceinline__ double operator()(int64_t t) const {
+    const double df = (double)x[t] - ct[t * k];
+    return df * df;
+  }
+};
+
 // Register-resident exact distance for d <= MAXD (MAXD multiple of 8):
 // numpy's pairwise order specialised to n <= 128.  c may point to LDS.
 template <int MAXD, class CPTR>

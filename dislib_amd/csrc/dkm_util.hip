@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ C,
   for (int64_t t = threadIdx.x; t < dpad; t += blockDim.x) {
     const double val = t < d ? row[t] : 0.0;
     v.c32[c * dpad + t] = (float)val;
-    if ((flags & DKM_PREP_CSR) && t < d) v.ct64[t * k + c] = val;
+    if (t < d) v.ct64[t * k + c] = val;  // C^T: re-check and CSR kernels
   }
   if (threadIdx.x == 0) {
     // sequential over t: sklearn row_norms(squared=True) order

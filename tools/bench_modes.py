@@ -47,6 +47,7 @@ def main():
     modes = a.modes.split(",")
     lab = {m: torch.empty(a.n, dtype=torch.int32, device=dev) for m in modes}
     times = {m: [] for m in modes}
+    ptimes = {m: [] for m in modes}
     rech = {}
     for r in range(a.rounds):
         for m in modes:
@@ -60,6 +61,11 @@ def main():
             torch.cuda.synchronize()
             times[m].append(e0.elapsed_time(e1))
             rech[m] = _device.rechecked(ws) - before
+            e0.record()
+            _device.predict(dd, C, ws, lab[m], _MODES[m])
+            e1.record()
+            torch.cuda.synchronize()
+            ptimes[m].append(e0.elapsed_time(e1))
     ref = lab[modes[0]].cpu().numpy()
     out = {}
     bytes_ = a.n * a.d * (4 if a.fp32 else 8)
@@ -67,6 +73,7 @@ def main():
         t = np.array(times[m])
         same = bool(np.array_equal(lab[m].cpu().numpy(), ref))
         out[m] = {"median_ms": float(np.median(t)), "min_ms": float(t.min()),
+                  "predict_median_ms": float(np.median(ptimes[m])),
                   "GBps": bytes_ / (np.median(t) * 1e-3) / 1e9,
                   "rechecked": rech[m], "labels_equal_first": same}
     print(json.dumps({"n": a.n, "d": a.d, "k": a.k, "fp32": a.fp32,
