@@ -41,7 +41,7 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
   b += round_up(k * 4, 256);          // cn32
   b += round_up(k * 8, 256);          // cn64
   b += round_up(k * d * 8, 256);      // ct64
-  b += round_up(kpad16(k) * dpad16(d) * 4, 256);  // cfrag
+  b += round_up(kpad16(k) * dpad32(d) * 4, 256);  // cfrag
   b += round_up(kpad16(k) * 4, 256);  // cnpad
   b += round_up(kpad16(k) * dpad32(d) * 4, 256);  // bfrag (hi + lo bf16)
   b += round_up(n_queue * 4, 256);    // queue
@@ -63,7 +63,7 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   v->ct64 = (double *)p;
   p += round_up(k * d * 8, 256);
   v->cfrag = (float *)p;
-  p += round_up(kpad16(k) * dpad16(d) * 4, 256);
+  p += round_up(kpad16(k) * dpad32(d) * 4, 256);
   v->cnpad = (float *)p;
   p += round_up(kpad16(k) * 4, 256);
   v->bfrag = (uint16_t *)p;
@@ -117,47 +117,37 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ C,
   }
 }
 
-// Centres in MFMA A-fragment order for v_mfma_f32_16x16x4_f32 (dkm_dense):
-// block (cb, db) = 16 centres x 16 dims = 1 KB; lane l of a wave reads the
-// float4 at l*16 B: centre cb*16 + (l & 15), dims db*16 + 4*(l >> 4) + m,
-// m = 0..3 (one value per MFMA k-step m).  Zero padded; cnpad = +inf pads.
+// Centres in MFMA A-fragment order (dkm_dense k_screen).  Block (cb, ks) =
+// 16 centres x 32 features = 2 KB.  Lane l of a wave stands for centre
+// cb*16 + (l & 15) and features ks*32 + 8*(l >> 4) + m, m = 0..7:
+//  cfrag: 8 fp32 at l*32 B (v_mfma_f32_16x16x4_f32, k-step m);
+//  bfrag: 8 bf16 hi at l*16 B, 8 bf16 lo at 1024 + l*16 B
+//         (v_mfma_f32_16x16x32_bf16).
+// Zero padded; cnpad = +inf for padding centres.
 __global__ void __launch_bounds__(256) k_frag(const double *__restrict__ C,
                                               int64_t k, int64_t d, WsView v) {
-  const int64_t nkb = kpad16(k) / 16, ndb = dpad16(d) / 16;
-  const int64_t total = nkb * ndb * 256;
+  const int64_t nkb = kpad16(k) / 16, nks = dpad32(d) / 32;
+  const int64_t total = nkb * nks * 512;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t blk = e >> 8, w = e & 255;
-    const int64_t cb = blk / ndb, db = blk - cb * ndb;
-    const int l = (int)(w >> 2), m = (int)(w & 3);
+    const int64_t blk = e >> 9, w = e & 511;
+    const int64_t cb = blk / nks, ks = blk - cb * nks;
+    const int l = (int)(w >> 3), m = (int)(w & 7);
     const int64_t c = cb * 16 + (l & 15);
-    const int64_t t = db * 16 + 4 * (l >> 4) + m;
-    v.cfrag[e] = (c < k && t < d) ? (float)C[c * d + t] : 0.0f;
+    const int64_t t = ks * 32 + 8 * (l >> 4) + m;
+    const double x = (c < k && t < d) ? C[c * d + t] : 0.0;
+    v.cfrag[blk * 512 + l * 8 + m] = (float)x;
+    // bf16x3 split: c = hi + lo + O(2^-16 |c|), hi = bf16(c), lo = bf16(c-hi)
+    const __bf16 hi = (__bf16)(float)x;
+    const __bf16 lo = (__bf16)(float)(x - (double)(float)hi);
+    uint16_t *dst = v.bfrag + blk * 1024;
+    dst[l * 8 + m] = __builtin_bit_cast(uint16_t, hi);
+    dst[512 + l * 8 + m] = __builtin_bit_cast(uint16_t, lo);
   }
   const int64_t kp = kpad16(k);
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < kp;
        c += (int64_t)gridDim.x * blockDim.x)
     v.cnpad[c] = c < k ? v.cn32[c] : INFINITY;
-  // bf16x3 split: c = hi + lo + O(2^-16 |c|), hi = bf16(c), lo = bf16(c-hi).
-  // Block (cb, ks) = 16 centres x 32 features: [hi 1 KB | lo 1 KB]; lane l
-  // holds centre cb*16 + (l & 15), features ks*32 + 8*(l >> 4) + jj, jj<8
-  // (the A operand of v_mfma_f32_16x16x32_bf16).
-  const int64_t nks = dpad32(d) / 32;
-  const int64_t tot2 = nkb * nks * 512;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot2;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t blk = e >> 9, w = e & 511;
-    const int64_t cb = blk / nks, ks = blk - cb * nks;
-    const int l = (int)(w >> 3), jj = (int)(w & 7);
-    const int64_t c = cb * 16 + (l & 15);
-    const int64_t t = ks * 32 + 8 * (l >> 4) + jj;
-    const double x = (c < k && t < d) ? C[c * d + t] : 0.0;
-    const __bf16 hi = (__bf16)(float)x;
-    const __bf16 lo = (__bf16)(float)(x - (double)(float)hi);
-    uint16_t *dst = v.bfrag + blk * 1024;
-    dst[l * 8 + jj] = __builtin_bit_cast(uint16_t, hi);
-    dst[512 + l * 8 + jj] = __builtin_bit_cast(uint16_t, lo);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -296,8 +286,7 @@ int dkm_prepare_centers(const double *C, int64_t k, int64_t d, int flags,
   k_ws_header<<<1, 64, 0, s>>>(v.hdr, k, d, dpad, nq);
   k_prepare<<<(unsigned)k, 256, 0, s>>>(C, k, d, dpad, flags, v);
   {
-    const int64_t tot = std::max((kpad16(k) / 16) * (dpad16(d) / 16) * 256,
-                                 (kpad16(k) / 16) * (dpad32(d) / 32) * 512);
+    const int64_t tot = (kpad16(k) / 16) * (dpad32(d) / 32) * 512;
     const int64_t g = std::max<int64_t>(1, std::min<int64_t>((tot + 255) / 256,
                                                             4096));
     k_frag<<<(unsigned)g, 256, 0, s>>>(C, k, d, v);
