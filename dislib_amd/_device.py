@@ -175,6 +175,23 @@ def partial_sum(dd, C, ws, labels, acc, mode):
                "dkm_partial_sum")
 
 
+def assign_delta(dd, C, ws, labels, delta, mode):
+    """Incremental assignment (dense only): labels in/out, delta +=."""
+    so = _lib.lib()
+    k = C.shape[0]
+    fn = so.dkm_assign_delta_f32 if dd.dtype == np.float32 else \
+        so.dkm_assign_delta_f64
+    _lib.check(fn(ptr(dd.X), dd.n, dd.d, dd.X.stride(0), ptr(C), k, ws.p,
+                  ws.nbytes, ptr(labels), ptr(delta), mode, stream_ptr()),
+               "dkm_assign_delta")
+
+
+def add_(y, x):
+    so = _lib.lib()
+    _lib.check(so.dkm_add_f64(ptr(y), ptr(x), y.numel(), stream_ptr()),
+               "dkm_add_f64")
+
+
 def predict(dd, C, ws, labels, mode):
     so = _lib.lib()
     k = C.shape[0]

@@ -26,6 +26,8 @@ tree).  Extra keyword-only arguments select the assignment arithmetic
 (``mode``: "auto" | "exact" | "screen32" | "bf16x3", identical labels) and
 the device.
 """
+import os
+
 import numpy as np
 from scipy.sparse import csr_matrix, issparse
 
@@ -129,16 +131,24 @@ class KMeans:
         host = state.centers_host()
         self.centers = csr_matrix(host) if sparse else host
         self.n_iter = iteration
-        if set_labels:
-            state.attach_labels()
+        state.attach_labels()
+
+
+REFRESH = int(os.environ.get("DKM_REFRESH", "8"))
 
 
 class _Lloyd:
-    """Device state of one fit: resident data, centres, workspace and the
-    packed [sums | counts] accumulator.  ``step()`` is one Lloyd iteration:
-    prepare -> fused assign+accumulate -> all-reduce (multi-GPU) -> update +
-    criterion, then one 4-byte flag read (the reference's per-iteration sync
-    at base.py:143)."""
+    """Device state of one fit: resident data, centres, labels, workspace and
+    the packed [sums | counts] of the current assignment (``state``).
+
+    ``step()`` is one Lloyd iteration: prepare -> fused assignment (HIP) ->
+    all-reduce of the per-rank buffer (RCCL when N > 1) -> centre update +
+    criterion (HIP) -> one 4-byte flag read (the reference's per-iteration
+    sync, base.py:143).  Dense data uses the incremental assignment
+    (dkm_assign_delta: only samples whose label changed move their row
+    between clusters) and recomputes ``state`` from scratch
+    (dkm_partial_sum) on the first and every REFRESH-th iteration, which
+    bounds the rounding drift of the running sums."""
 
     def __init__(self, dataset, centers, tol, set_labels, mode="auto",
                  device=None, broadcast_init=False):
@@ -157,10 +167,13 @@ class _Lloyd:
             _shard.broadcast_(self.C)     # ranks must start identically
         self.ws = Workspace(k, d, max(1, min(dd.n, 1 << 27)), dd.device)
         self.acc = t.empty(k * (d + 1), dtype=t.float64, device=dd.device)
+        self.state = t.zeros(k * (d + 1), dtype=t.float64, device=dd.device)
         self.diff = t.zeros(k + 1, dtype=t.float64, device=dd.device)
         self.flag = t.zeros(1, dtype=t.int32, device=dd.device)
-        self.labels = t.empty(max(dd.n, 1), dtype=t.int32, device=dd.device) \
-            if set_labels else None
+        self.labels = t.full((max(dd.n, 1),), -1, dtype=t.int32,
+                             device=dd.device)
+        self.set_labels = set_labels
+        self.it = 0
         if self.sparse:
             self.sums_mode = _lib.SUMS_RECIP
         elif dd.dtype == np.float32:
@@ -175,23 +188,37 @@ class _Lloyd:
         from .._device import prepare
         prepare(self.C, self.ws, self.acc, csr=self.sparse)
 
+    def _full(self):
+        return self.sparse or self.it % REFRESH == 0
+
     def partial(self):
-        """Fused assignment + partial sums over all resident samples (the
-        hot kernel: dkm_partial_sum_*)."""
-        from .._device import partial_sum
-        if self.dd.n > 0:
+        """The hot kernel: fused assignment over all resident samples, full
+        partial sums (dkm_partial_sum_*) or incremental (dkm_assign_delta_*).
+        """
+        from .._device import assign_delta, partial_sum
+        if self.dd.n == 0:
+            return
+        if self._full():
             partial_sum(self.dd, self.C, self.ws, self.labels, self.acc,
                         self.mode)
+        else:
+            assign_delta(self.dd, self.C, self.ws, self.labels, self.acc,
+                         self.mode)
 
     def assign(self):
         self.prepare()
         self.partial()
 
     def reduce_update(self):
-        from .._device import update
+        from .._device import add_, update
         _shard.allreduce_sum_(self.acc)
-        update(self.acc, self.C, self.sums_mode, self.tol, self.diff,
+        if self._full():
+            self.state.copy_(self.acc)
+        else:
+            add_(self.state, self.acc)
+        update(self.state, self.C, self.sums_mode, self.tol, self.diff,
                self.flag)
+        self.it += 1
 
     def step(self):
         self.assign()
@@ -209,5 +236,5 @@ class _Lloyd:
         return self.C.cpu().numpy()
 
     def attach_labels(self):
-        if self.dd.n > 0:
+        if self.set_labels and self.dd.n > 0:
             self.dataset._attach_device_labels(self.labels[:self.dd.n])

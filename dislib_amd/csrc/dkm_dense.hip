@@ -10,18 +10,23 @@
 //   label  = first j with minimal dist_j      [np.argmin, base.py:173]
 //
 // Kernels
-//   k_exact_reg<MAXD>  lane = sample, x in VGPRs, centres (fp64) in LDS,
-//                      the exact numpy-order distance to every centre.
+//   k_exact_reg<MAXD>  lane = sample, x in VGPRs, centres (fp64) in LDS: the
+//                      reference arithmetic for every (sample, centre).
 //   k_exact_gen        lane = sample, any d, x/centres through the caches.
-//   k_screen<MAXD>     lane = sample, fp32 score s_j = |c_j|^2 - 2 x.c_j
-//                      against fp32 centres in LDS; a rigorous error bound
-//                      decides whether the fp32 winner is the exact winner.
-//                      Ambiguous samples are queued for ...
-//   k_recheck          wave = one queued sample, lanes = centres, exact
-//                      arithmetic, wave-wide (dist, index) argmin.
-// Sums/counts go to acc = [sums k*d | counts k] (fp64) through LDS-private
-// accumulators flushed once per block, or global fp64 atomics when they do
-// not fit.
+//   k_screen           MFMA screen: s_j = |c_j|^2 - 2 x.c_j (fp32 or bf16x3
+//                      split precision), a rigorous error bound decides
+//                      whether the screened winner IS the reference winner;
+//                      otherwise the label is left for ...
+//   k_recheck_scan     exact arithmetic for the undecided samples (wave per
+//                      sample, lanes over centres, coalesced C^T reads).
+//
+// Accumulation (acc = [sums k*d | counts k], fp64):
+//   AM_LDS / AM_GLOBAL  every sample adds its row (partial_sum semantics);
+//                       LDS-private accumulators (odd row stride) flushed
+//                       once per block, or fp64 global atomics.
+//   AM_DELTA            incremental: labels[] holds the previous assignment;
+//                       only samples whose label changes add +x to the new
+//                       and -x to the old cluster (dkm_assign_delta).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -35,7 +40,7 @@ namespace dkm {
 constexpr int BLOCK = 256;
 constexpr size_t LDS_BUDGET = 80 * 1024;  // per block -> >= 2 blocks / CU
 
-enum AccMode { ACC_NONE = 0, ACC_LDS = 1, ACC_GLOBAL = 2 };
+enum AccMode { AM_NONE = 0, AM_LDS = 1, AM_GLOBAL = 2, AM_DELTA = 3 };
 
 struct DevInfo {
   int cus = 256;
@@ -70,23 +75,34 @@ __host__ __device__ __forceinline__ int64_t lds_acc_len(int64_t k, int d) {
   return k * lds_stride(d) + k;
 }
 
-// Add a sample row to its cluster's sum (and count) -- lane-per-sample form.
+__device__ __forceinline__ void lds_add(double *p, double v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Accumulate one sample (lane-per-sample kernels).
 template <class TX>
 __device__ __forceinline__ void acc_row_lane(int amode, double *lds_acc,
                                              double *acc, int64_t k, int d,
-                                             int label, const TX *xrow) {
-  if (amode == ACC_LDS) {
+                                             int label, int prev,
+                                             const TX *xrow) {
+  if (amode == AM_LDS) {
     const int ds = lds_stride(d);
     double *srow = lds_acc + (int64_t)label * ds;
-    for (int t = 0; t < d; ++t)
-      __hip_atomic_fetch_add(srow + t, ld_x(xrow + t), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add(lds_acc + k * ds + label, 1.0, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-  } else if (amode == ACC_GLOBAL) {
+    for (int t = 0; t < d; ++t) lds_add(srow + t, ld_x(xrow + t));
+    lds_add(lds_acc + k * ds + label, 1.0);
+  } else if (amode == AM_GLOBAL) {
     double *srow = acc + (int64_t)label * d;
     for (int t = 0; t < d; ++t) atomic_add_f64(srow + t, ld_x(xrow + t));
     atomic_add_f64(acc + k * d + label, 1.0);
+  } else if (amode == AM_DELTA && label != prev) {
+    double *srow = acc + (int64_t)label * d;
+    for (int t = 0; t < d; ++t) atomic_add_f64(srow + t, ld_x(xrow + t));
+    atomic_add_f64(acc + k * d + label, 1.0);
+    if (prev >= 0) {
+      double *orow = acc + (int64_t)prev * d;
+      for (int t = 0; t < d; ++t) atomic_add_f64(orow + t, -ld_x(xrow + t));
+      atomic_add_f64(acc + k * d + prev, -1.0);
+    }
   }
 }
 
@@ -117,10 +133,10 @@ __global__ void __launch_bounds__(BLOCK)
                 double *acc, int amode) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double *cl = smem;                         // k*d centres
-  double *lds_acc = smem + (int64_t)k * d;   // k*(d+1) accumulators
+  double *lds_acc = smem + (int64_t)k * d;   // accumulators (AM_LDS)
   const int64_t kd = (int64_t)k * d;
   for (int64_t e = threadIdx.x; e < kd; e += blockDim.x) cl[e] = C[e];
-  if (amode == ACC_LDS) zero_lds_acc(lds_acc, k, d);
+  if (amode == AM_LDS) zero_lds_acc(lds_acc, k, d);
   __syncthreads();
 
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -146,10 +162,11 @@ __global__ void __launch_bounds__(BLOCK)
         best_s = s;
       }
     }
+    const int prev = (amode == AM_DELTA) ? labels[i] : -1;
     if (labels) labels[i] = bi;
-    acc_row_lane(amode, lds_acc, acc, k, d, bi, xr);
+    acc_row_lane(amode, lds_acc, acc, k, d, bi, prev, xr);
   }
-  if (amode == ACC_LDS) {
+  if (amode == AM_LDS) {
     __syncthreads();
     flush_lds_acc(lds_acc, acc, k, d);
   }
@@ -185,7 +202,7 @@ __global__ void __launch_bounds__(BLOCK)
                 double *acc, int amode) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double *lds_acc = smem;
-  if (amode == ACC_LDS) {
+  if (amode == AM_LDS) {
     zero_lds_acc(lds_acc, k, d);
     __syncthreads();
   }
@@ -194,53 +211,58 @@ __global__ void __launch_bounds__(BLOCK)
        i += stride) {
     const TX *xr = X + i * ldx;
     const int bi = exact_label_lane(xr, d, C, k);
+    const int prev = (amode == AM_DELTA) ? labels[i] : -1;
     if (labels) labels[i] = bi;
-    acc_row_lane(amode, lds_acc, acc, k, d, bi, xr);
+    acc_row_lane(amode, lds_acc, acc, k, d, bi, prev, xr);
   }
-  if (amode == ACC_LDS) {
+  if (amode == AM_LDS) {
     __syncthreads();
     flush_lds_acc(lds_acc, acc, k, d);
   }
 }
 
 // ---------------------------------------------------------------------------
-// MFMA screen: score s_j = |c_j|^2 - 2 x.c_j with matrix cores, a rigorous
+// MFMA screen.  Score s_j = |c_j|^2 - 2 x.c_j on matrix cores, a rigorous
 // bound B on |(s_j + |x|^2) - numpy_dist_j^2|, and the exact re-check of
 // every sample whose best two scores are not 2B apart.
 //
 // Precisions (PREC):
-//   P_F32  v_mfma_f32_16x16x4_f32 (exact f32 fma chains, x and c rounded to
-//          fp32).  Bound: conversions 2u|x.c|, the d-term chain d*u*sum|x c|,
-//          fp32 |c|^2 (u|c|^2) and the final fma (u|s|), u = 2^-24.
-//   P_B3   v_mfma_f32_16x16x32_bf16 on bf16 hi/lo splits:
-//          x.c ~ xh.ch + xh.cl + xl.ch; split remainder 3.1 * 2^-16 sum|x c|,
+//   P_F32  v_mfma_f32_16x16x4_f32 (exact f32 fma chains) on x32 = fl32(x),
+//          c32 = fl32(c).  Bound: conversions 2u|x.c|, the d-term chain
+//          d*u*sum|x c|, fp32 |c|^2 (u|c|^2), final fma (u|s|), u = 2^-24.
+//   P_B3   v_mfma_f32_16x16x32_bf16 on bf16 hi/lo splits of x32 and c:
+//          x.c ~ xh.ch + xh.cl + xl.ch (products exact in fp32); split
+//          remainder <= 3.1 * 2^-16 sum|x c| (incl. the x -> x32 rounding),
 //          fp32 accumulation of 3d products bounded as (3d + 6) roundings of
-//          2^-23 (conservative: no assumption about the MFMA's internal
-//          adder), fp32 |c|^2 and final fma.
-// Both: doubled for safety, plus numpy's fp64 rounding (16 * 2^-52 (|x| +
-// |c|)^2) and an absolute underflow floor; |x.c| <= |x| cmax.
+//          2^-23 (no assumption about the MFMA's internal adder), fp32
+//          |c|^2 and final fma.
+// Both doubled for safety, plus numpy's fp64 rounding (16 * 2^-52 (|x| +
+// cmax)^2), an absolute underflow floor, and |x.c| <= |x| cmax.  |x| is
+// computed in fp32 and inflated (relative error <= (d + 4) 2^-24).
 // ---------------------------------------------------------------------------
 enum { P_F32 = 0, P_B3 = 1 };
 
 template <int PREC>
-__device__ __forceinline__ double screen_bound(int d, double xn, double cm) {
-  double rel;
+__device__ __forceinline__ float screen_bound(int d, float xn, float cm) {
+  float rel;
   if (PREC == P_F32)
-    rel = (d + 6.0) * 0x1.0p-24;
+    rel = (d + 6.0f) * 0x1.0p-24f;
   else
-    rel = 3.1 * 0x1.0p-16 + (3.0 * d + 6.0) * 0x1.0p-23;
-  double b = 2.0 * rel * (2.0 * xn * cm + cm * cm);
-  b += 16.0 * 0x1.0p-52 * (xn + cm) * (xn + cm);
-  b += 8.0 * sqrt((double)d) * 0x1.0p-120 * (xn + cm + 1.0) + d * 0x1.0p-120;
-  return b;
+    rel = 3.1f * 0x1.0p-16f + (3.0f * d + 6.0f) * 0x1.0p-23f;
+  const float s = xn + cm;
+  float b = 2.0f * rel * (2.0f * xn * cm + cm * cm);
+  b += 16.0f * 0x1.0p-52f * s * s;
+  b += (8.0f * d) * 0x1.0p-120f * (s + 1.0f);
+  return b * 1.0001f;  // covers the fp32 evaluation of this bound
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int SB = 256;  // screen block: 4 waves
 
-// Eight consecutive features t0..t0+7 of one row as fp64.  VEC: d % 8 == 0
+// Eight consecutive features t0..t0+7 of one row, as fp64.  VEC: d % 8 == 0
 // and 16-B aligned rows, so the 8 features are in range iff t0 < d.
 template <bool VEC, class TX>
 __device__ __forceinline__ void load8(const TX *xr, int t0, int d,
@@ -271,13 +293,15 @@ __device__ __forceinline__ void load8(const TX *xr, int t0, int d,
 
 // One wave = NB blocks of 16 samples per step.  Lane l = (q = l >> 4,
 // j = l & 15) holds features ks*32 + 8q + m (m < 8) of sample j of every
-// block: each load pair reads 16 rows x 64 B, every 128-B line whole within
-// the four load instructions of a 32-feature block.  The next step's rows
-// are loaded while the current step computes (registers, double buffer).
-// The MFMA output gives lane (q, j) the dots of centres cb*16 + 4q + i
-// (i < 4) with sample j; each lane keeps a top-2, two xor-shuffles merge the
-// four lanes of a sample.  lab_out[si] = label, or -1 when the screen cannot
-// decide (k_recheck_scan then computes it exactly).
+// block (4 x 16-B loads per lane per 32 features).  Outside the full-
+// accumulation modes the fp64 tile registers are reloaded with the NEXT
+// step's rows as soon as they are converted, so one tile is in flight during
+// the MFMA/scoring of the current one.  The MFMA output gives lane (q, j)
+// the dots of centres cb*16 + 4q + i (i < 4) with sample j; each lane keeps a
+// top-2 (fma, cmp, cndmask, med3, min per score), two xor-shuffles merge the
+// four lanes of a sample.  lab_out[si] = label, or -(prev + 2) when the
+// screen cannot decide (k_recheck_scan computes it exactly; prev = -1
+// outside AM_DELTA).
 template <int PREC, int NKS, int NB, bool VEC, class TX>
 __global__ void __launch_bounds__(SB)
     k_screen(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
@@ -296,18 +320,20 @@ __global__ void __launch_bounds__(SB)
     f32x4 *dst = (f32x4 *)frag;
     for (int e = threadIdx.x; e < nkb * NKS * 128; e += SB) dst[e] = src[e];
     for (int e = threadIdx.x; e < nkb * 16; e += SB) cn[e] = v.cnpad[e];
-    if (amode == ACC_LDS) zero_lds_acc(lds_acc, k, d);
+    if (amode == AM_LDS) zero_lds_acc(lds_acc, k, d);
   }
-  const double cm = __longlong_as_double((long long)v.hdr->cmax_bits);
+  const float cm =
+      (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
   const int ds = lds_stride(d);
+  const bool full_acc = (amode == AM_LDS || amode == AM_GLOBAL);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
   const int64_t wv = (int64_t)blockIdx.x * (SB / 64) + (threadIdx.x >> 6);
   const int64_t step = (int64_t)gridDim.x * (SB / 64) * 16 * NB;
 
-  double cur[NB][NKS][8], nxt[NB][NKS][8];
-  auto load_tile = [&](int64_t s0, double (&t)[NB][NKS][8]) {
+  double tile[NB][NKS][8];
+  auto load_tile = [&](int64_t s0) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       int64_t si = s0 + 16 * b + j;
@@ -315,38 +341,40 @@ __global__ void __launch_bounds__(SB)
       const TX *xr = X + si * ldx;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
-        load8<VEC>(xr, ks * 32 + 8 * q, d, t[b][ks]);
+        load8<VEC>(xr, ks * 32 + 8 * q, d, tile[b][ks]);
     }
   };
 
   int64_t s0 = base + wv * 16 * NB;
-  if (s0 < n) load_tile(s0, cur);
+  if (s0 < n) load_tile(s0);
   for (; s0 < n; s0 += step) {
-    if (s0 + step < n) load_tile(s0 + step, nxt);
-
-    double xx[NB];
+    // ---- convert the tile (fp64 -> fp32 -> operands), |x|^2 in fp32 ----
+    float xx[NB];
     float xf[PREC == P_F32 ? NB : 1][NKS][8];
     bf16x8 xh[PREC == P_B3 ? NB : 1][NKS], xl[PREC == P_B3 ? NB : 1][NKS];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      xx[b] = 0.0;
+      xx[b] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
-          const double x = cur[b][ks][m];
-          xx[b] = fma(x, x, xx[b]);
+          const float x32 = (float)tile[b][ks][m];
+          xx[b] = fmaf(x32, x32, xx[b]);
           if constexpr (PREC == P_F32) {
-            xf[b][ks][m] = (float)x;
+            xf[b][ks][m] = x32;
           } else {
-            const __bf16 h = (__bf16)(float)x;
+            const __bf16 h = (__bf16)x32;
             xh[b][ks][m] = h;
-            xl[b][ks][m] = (__bf16)(float)(x - (double)(float)h);
+            xl[b][ks][m] = (__bf16)(x32 - (float)h);  // exact subtraction
           }
         }
       xx[b] += __shfl_xor(xx[b], 16, WAVE);
       xx[b] += __shfl_xor(xx[b], 32, WAVE);
     }
+    // ---- the next step's rows stream in while this one computes ----
+    const int64_t s_next = s0 + step;
+    if (!full_acc && s_next < n) load_tile(s_next);
 
     float b1[NB], b2[NB];
     int i1[NB];
@@ -392,16 +420,28 @@ __global__ void __launch_bounds__(SB)
       }
       const float4 cn4 = *(const float4 *)(cn + cb * 16 + 4 * q);
       const float cnv[4] = {cn4.x, cn4.y, cn4.z, cn4.w};
+      const int cbase = cb * 16 + 4 * q;
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
+      for (int i = 0; i < 4; ++i) {
+        float sc[NB];
+        if constexpr (NB == 2) {
+          const f32x2 s2 = __builtin_elementwise_fma(
+              f32x2{accv[0][i], accv[1][i]}, f32x2{-2.f, -2.f},
+              f32x2{cnv[i], cnv[i]});
+          sc[0] = s2.x;
+          sc[1] = s2.y;
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float sc = fmaf(-2.f, accv[b][i], cnv[i]);
-          const bool lt = sc < b1[b];
-          b2[b] = lt ? b1[b] : fminf(b2[b], sc);
-          i1[b] = lt ? cb * 16 + 4 * q + i : i1[b];
-          b1[b] = lt ? sc : b1[b];
+          for (int b = 0; b < NB; ++b) sc[b] = fmaf(-2.f, accv[b][i], cnv[i]);
         }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          // b1 <= b2: new second = med3(b1, b2, s); ties -> b2 == b1
+          i1[b] = sc[b] < b1[b] ? cbase + i : i1[b];
+          b2[b] = __builtin_amdgcn_fmed3f(b1[b], b2[b], sc[b]);
+          b1[b] = fminf(b1[b], sc[b]);
+        }
+      }
     }
     // merge the top-2 of the four lanes of a sample (first index on ties)
 #pragma unroll
@@ -411,68 +451,78 @@ __global__ void __launch_bounds__(SB)
         const float ob1 = __shfl_xor(b1[b], off, WAVE);
         const float ob2 = __shfl_xor(b2[b], off, WAVE);
         const int oi1 = __shfl_xor(i1[b], off, WAVE);
-        if (ob1 < b1[b] || (ob1 == b1[b] && oi1 < i1[b])) {
-          b2[b] = fminf(b1[b], ob2);
-          b1[b] = ob1;
-          i1[b] = oi1;
-        } else {
-          b2[b] = fminf(b2[b], ob1);
-        }
+        const bool other = ob1 < b1[b] || (ob1 == b1[b] && oi1 < i1[b]);
+        b2[b] = other ? fminf(b1[b], ob2) : fminf(b2[b], ob1);
+        i1[b] = other ? oi1 : i1[b];
+        b1[b] = other ? ob1 : b1[b];
       }
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int64_t si = s0 + 16 * b + j;
       if (si >= n) continue;
-      const double xn = sqrt(xx[b]);
-      const double B = screen_bound<PREC>(d, xn, cm);
-      const bool sane = (xn < 1e18) && (xn * cm < 1e30);
-      const bool unique = sane && ((double)b2[b] - (double)b1[b] > 2.0 * B);
-      if (q == 0) lab_out[si] = unique ? i1[b] : -1;
-      if (!unique) continue;  // label + sums by k_recheck_scan
+      const float xn = sqrtf(xx[b]) * (1.0f + (d + 4) * 0x1.0p-24f);
+      const float B = screen_bound<PREC>(d, xn, cm);
+      const bool sane = (xn < 1e18f) && (xn * cm < 1e30f);
+      const bool unique = sane && (b2[b] - b1[b] > 2.0f * B);
       const int lab = i1[b];
-      if (amode == ACC_LDS) {
+      int prev = -1;
+      if (amode == AM_DELTA) prev = lab_out[si];  // 16 lanes x 4 B, coalesced
+      if (q == 0) lab_out[si] = unique ? lab : -(prev + 2);
+      if (!unique) continue;  // label + sums by k_recheck_scan
+      if (amode == AM_LDS) {
         double *srow = lds_acc + (int64_t)lab * ds;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
           for (int m = 0; m < 8; ++m) {
             const int t = ks * 32 + 8 * q + m;
-            if (t < d)
-              __hip_atomic_fetch_add(srow + t, cur[b][ks][m], __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (t < d) lds_add(srow + t, tile[b][ks][m]);
           }
-        if (q == 0)
-          __hip_atomic_fetch_add(lds_acc + (int64_t)k * ds + lab, 1.0,
-                                 __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else if (amode == ACC_GLOBAL) {
+        if (q == 0) lds_add(lds_acc + (int64_t)k * ds + lab, 1.0);
+      } else if (amode == AM_GLOBAL) {
         double *srow = acc + (int64_t)lab * d;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
           for (int m = 0; m < 8; ++m) {
             const int t = ks * 32 + 8 * q + m;
-            if (t < d) atomic_add_f64(srow + t, cur[b][ks][m]);
+            if (t < d) atomic_add_f64(srow + t, tile[b][ks][m]);
           }
         if (q == 0) atomic_add_f64(acc + (int64_t)k * d + lab, 1.0);
+      } else if (amode == AM_DELTA && lab != prev) {
+        // rare after the first iterations: reload the row (L2) and move it
+        const TX *xr = X + si * ldx;
+        double *nrow = acc + (int64_t)lab * d;
+        double *orow = acc + (int64_t)(prev < 0 ? 0 : prev) * d;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+          for (int m = 0; m < 8; ++m) {
+            const int t = ks * 32 + 8 * q + m;
+            if (t < d) {
+              const double x = ld_x(xr + t);
+              atomic_add_f64(nrow + t, x);
+              if (prev >= 0) atomic_add_f64(orow + t, -x);
+            }
+          }
+        if (q == 0) {
+          atomic_add_f64(acc + (int64_t)k * d + lab, 1.0);
+          if (prev >= 0) atomic_add_f64(acc + (int64_t)k * d + prev, -1.0);
+        }
       }
     }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-        for (int m = 0; m < 8; ++m) cur[b][ks][m] = nxt[b][ks][m];
+    if (full_acc && s_next < n) load_tile(s_next);  // the tile was in use
   }
-  if (amode == ACC_LDS) {
+  if (amode == AM_LDS) {
     __syncthreads();
     flush_lds_acc(lds_acc, acc, k, d);
   }
 }
 
-// Exact re-check of the samples the screen left at -1: each wave scans 64
-// labels at a time (coalesced), and for every -1 computes the reference
+// Exact re-check of the samples the screen left undecided (lab_out < 0,
+// encoding the previous label as -(prev + 2)): each wave scans 64 labels at
+// a time (coalesced), and for every undecided one computes the reference
 // distance to all centres (lanes over centres, C^T reads coalesced), the
 // (dist, index) argmin, the label and the sums.  No shared counter.
 template <bool SMALL, class TX>
@@ -484,7 +534,7 @@ __global__ void __launch_bounds__(BLOCK)
   double *lds_acc = smem;
   __shared__ unsigned long long blk_count;
   if (threadIdx.x == 0) blk_count = 0;
-  if (amode == ACC_LDS) zero_lds_acc(lds_acc, k, d);
+  if (amode == AM_LDS) zero_lds_acc(lds_acc, k, d);
   __syncthreads();
   const int ds = lds_stride(d);
   const int lane = threadIdx.x & 63;
@@ -500,6 +550,7 @@ __global__ void __launch_bounds__(BLOCK)
       const int bit = __ffsll((long long)mask) - 1;
       mask &= mask - 1;
       const int64_t i = c0 + bit;
+      const int prev = -__shfl(lv, bit, WAVE) - 2;
       const TX *xr = X + i * ldx;
       double best = INFINITY;
       int bi = 0x7fffffff;  // lanes without a centre never win
@@ -514,19 +565,22 @@ __global__ void __launch_bounds__(BLOCK)
       }
       wave_argmin(best, bi);
       if (lane == 0) lab_out[i] = bi;
-      if (amode == ACC_LDS) {
+      if (amode == AM_LDS) {
         for (int t = lane; t < d; t += 64)
-          __hip_atomic_fetch_add(lds_acc + (int64_t)bi * ds + t, ld_x(xr + t),
-                                 __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (lane == 0)
-          __hip_atomic_fetch_add(lds_acc + (int64_t)k * ds + bi, 1.0,
-                                 __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else if (amode == ACC_GLOBAL) {
-        for (int t = lane; t < d; t += 64)
-          atomic_add_f64(acc + (int64_t)bi * d + t, ld_x(xr + t));
-        if (lane == 0) atomic_add_f64(acc + (int64_t)k * d + bi, 1.0);
+          lds_add(lds_acc + (int64_t)bi * ds + t, ld_x(xr + t));
+        if (lane == 0) lds_add(lds_acc + (int64_t)k * ds + bi, 1.0);
+      } else if (amode == AM_GLOBAL || (amode == AM_DELTA && bi != prev)) {
+        for (int t = lane; t < d; t += 64) {
+          const double x = ld_x(xr + t);
+          atomic_add_f64(acc + (int64_t)bi * d + t, x);
+          if (amode == AM_DELTA && prev >= 0)
+            atomic_add_f64(acc + (int64_t)prev * d + t, -x);
+        }
+        if (lane == 0) {
+          atomic_add_f64(acc + (int64_t)k * d + bi, 1.0);
+          if (amode == AM_DELTA && prev >= 0)
+            atomic_add_f64(acc + (int64_t)k * d + prev, -1.0);
+        }
       }
     }
   }
@@ -536,7 +590,14 @@ __global__ void __launch_bounds__(BLOCK)
   __syncthreads();
   if (threadIdx.x == 0 && blk_count)
     atomicAdd((unsigned long long *)&v.hdr->rechecked_total, blk_count);
-  if (amode == ACC_LDS) flush_lds_acc(lds_acc, acc, k, d);
+  if (amode == AM_LDS) flush_lds_acc(lds_acc, acc, k, d);
+}
+
+__global__ void k_add(double *__restrict__ y, const double *__restrict__ x,
+                      int64_t n) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x)
+    y[e] += x[e];
 }
 
 // ---------------------------------------------------------------------------
@@ -547,42 +608,43 @@ static int pick_maxd(int d) {
   if (d <= 16) return 16;
   if (d <= 32) return 32;
   if (d <= 64) return 64;
-  if (d <= 128) return 128;
   return 0;
 }
 
-static unsigned grid_for(int64_t n, const void *kern, size_t lds) {
+static unsigned grid_for(int64_t n, const void *kern, int block, size_t lds) {
   int per_cu = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BLOCK,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block,
                                                    lds) != hipSuccess ||
       per_cu < 1)
     per_cu = 1;
   const int64_t cap = (int64_t)dev_info().cus * per_cu;
-  const int64_t need = (n + BLOCK - 1) / BLOCK;
+  const int64_t need = (n + block - 1) / block;
   return (unsigned)std::max<int64_t>(1, std::min(need, cap));
 }
 
+// acc_kind: 0 = none (predict), 1 = full accumulation, 2 = delta
 template <class TX>
 static int launch_exact(const TX *X, int64_t n, int d, int64_t ldx,
                         const double *C, int k, int32_t *labels, double *acc,
-                        hipStream_t s) {
+                        int acc_kind, hipStream_t s) {
   const int64_t kd = (int64_t)k * d;
   const size_t c_bytes = (size_t)kd * 8;
   const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
   const int maxd = pick_maxd(d);
-  const bool creg = maxd > 0 && maxd <= 64 && c_bytes <= LDS_BUDGET;
-  int amode = ACC_NONE;
-  if (acc) {
+  const bool creg = maxd > 0 && c_bytes <= LDS_BUDGET;
+  int amode = AM_NONE;
+  if (acc_kind == 2) {
+    amode = AM_DELTA;
+  } else if (acc_kind == 1) {
     const size_t base = creg ? c_bytes : 0;
-    amode = (base + a_bytes <= LDS_BUDGET) ? ACC_LDS : ACC_GLOBAL;
+    amode = (base + a_bytes <= LDS_BUDGET) ? AM_LDS : AM_GLOBAL;
   }
-  const size_t lds =
-      (creg ? c_bytes : 0) + (amode == ACC_LDS ? a_bytes : 0);
+  const size_t lds = (creg ? c_bytes : 0) + (amode == AM_LDS ? a_bytes : 0);
   if (creg) {
 #define DKM_EXACT_CASE(M)                                                   \
   case M: {                                                                 \
     const void *kf = (const void *)k_exact_reg<M, TX>;                      \
-    unsigned g = grid_for(n, kf, lds);                                      \
+    unsigned g = grid_for(n, kf, BLOCK, lds);                               \
     k_exact_reg<M, TX><<<g, BLOCK, lds, s>>>(X, n, d, ldx, C, k, labels,    \
                                              acc, amode);                   \
     break;                                                                  \
@@ -596,7 +658,7 @@ static int launch_exact(const TX *X, int64_t n, int d, int64_t ldx,
 #undef DKM_EXACT_CASE
   } else {
     const void *kf = (const void *)k_exact_gen<TX>;
-    unsigned g = grid_for(n, kf, lds);
+    unsigned g = grid_for(n, kf, BLOCK, lds);
     k_exact_gen<TX><<<g, BLOCK, lds, s>>>(X, n, d, ldx, C, k, labels, acc,
                                           amode);
   }
@@ -662,13 +724,16 @@ static int launch_screen_nks(const TX *X, int64_t end, int d, int64_t ldx,
 template <class TX>
 static int launch_recheck_scan(const TX *X, int64_t end, int d, int64_t ldx,
                                int k, const WsView &v, int32_t *lab_out,
-                               double *acc, int64_t base, hipStream_t s) {
-  int amode = ACC_NONE;
+                               double *acc, int acc_kind, int64_t base,
+                               hipStream_t s) {
+  int amode = AM_NONE;
   size_t lds = 0;
-  if (acc) {
+  if (acc_kind == 2) {
+    amode = AM_DELTA;
+  } else if (acc_kind == 1) {
     const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
-    amode = a_bytes <= LDS_BUDGET ? ACC_LDS : ACC_GLOBAL;
-    lds = amode == ACC_LDS ? a_bytes : 0;
+    amode = a_bytes <= LDS_BUDGET ? AM_LDS : AM_GLOBAL;
+    lds = amode == AM_LDS ? a_bytes : 0;
   }
   const int64_t waves = (end - base + 63) / 64;
   const unsigned g = (unsigned)std::max<int64_t>(
@@ -688,7 +753,8 @@ static int launch_recheck_scan(const TX *X, int64_t end, int d, int64_t ldx,
 template <class TX>
 static int launch_screen(int prec, const TX *X, int64_t n, int d,
                          int64_t ldx, int k, const WsView &v, size_t wsb,
-                         int32_t *labels, double *acc, hipStream_t s) {
+                         int32_t *labels, double *acc, int acc_kind,
+                         hipStream_t s) {
   const size_t fixed = (size_t)((const char *)v.queue - (const char *)v.hdr);
   const int64_t nq =
       std::min<int64_t>((int64_t)((wsb - fixed) / 4), INT32_MAX);
@@ -697,9 +763,12 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const int64_t chunk = labels ? n : nq;
   const size_t fb = screen_lds_fixed(k, d);
   const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
-  int amode = ACC_NONE;
-  if (acc) amode = (fb + a_bytes <= LDS_BUDGET) ? ACC_LDS : ACC_GLOBAL;
-  const size_t lds = fb + (amode == ACC_LDS ? a_bytes : 0);
+  int amode = AM_NONE;
+  if (acc_kind == 2)
+    amode = AM_DELTA;
+  else if (acc_kind == 1)
+    amode = (fb + a_bytes <= LDS_BUDGET) ? AM_LDS : AM_GLOBAL;
+  const size_t lds = fb + (amode == AM_LDS ? a_bytes : 0);
   const bool vec = (d % 8 == 0) && (ldx % (16 / (int64_t)sizeof(TX)) == 0) &&
                    (((uintptr_t)X % 16) == 0);
   for (int64_t base = 0; base < n; base += chunk) {
@@ -721,8 +790,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                                                    lab_out, acc, amode, base,
                                                    lds, s);
     if (r) return r;
-    if ((r = launch_recheck_scan<TX>(X, end, d, ldx, k, v, lab_out, acc, base,
-                                     s)))
+    if ((r = launch_recheck_scan<TX>(X, end, d, ldx, k, v, lab_out, acc,
+                                     acc_kind, base, s)))
       return r;
   }
   return 0;
@@ -731,8 +800,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
 template <class TX>
 static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                   const double *C, int64_t k, const void *ws, size_t wsb,
-                  int32_t *labels, double *acc, int mode, void *stream,
-                  const char *who) {
+                  int32_t *labels, double *acc, int acc_kind, int mode,
+                  void *stream, const char *who) {
   if (n < 0 || d <= 0 || k <= 0 || ldx < d)
     return fail(DKM_E_ARG, std::string(who) + ": bad n/d/k/ldx");
   if (d > INT32_MAX || k > INT32_MAX)
@@ -745,14 +814,17 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
   if (mode == DKM_MODE_AUTO)
     mode = screen_ok(k, d) ? DKM_MODE_SCREEN_BF16X3 : DKM_MODE_EXACT;
   if (mode == DKM_MODE_EXACT)
-    return launch_exact<TX>(X, n, (int)d, ldx, C, (int)k, labels, acc, s);
+    return launch_exact<TX>(X, n, (int)d, ldx, C, (int)k, labels, acc,
+                            acc_kind, s);
   if (mode == DKM_MODE_SCREEN32 || mode == DKM_MODE_SCREEN_BF16X3) {
     if (!screen_ok(k, d))
-      return launch_exact<TX>(X, n, (int)d, ldx, C, (int)k, labels, acc, s);
+      return launch_exact<TX>(X, n, (int)d, ldx, C, (int)k, labels, acc,
+                              acc_kind, s);
     WsView v;
     if (int r = ws_view(ws, wsb, k, d, &v)) return r;
     return launch_screen<TX>(mode == DKM_MODE_SCREEN32 ? P_F32 : P_B3, X, n,
-                             (int)d, ldx, (int)k, v, wsb, labels, acc, s);
+                             (int)d, ldx, (int)k, v, wsb, labels, acc,
+                             acc_kind, s);
   }
   return fail(DKM_E_ARG, std::string(who) + ": bad mode");
 }
@@ -768,8 +840,8 @@ int dkm_partial_sum_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
                         size_t ws_bytes, int32_t *labels, double *acc,
                         int mode, void *stream) {
   if (!acc) return fail(DKM_E_ARG, "partial_sum: acc is NULL");
-  return assign<double>(X, n, d, ldx, C, k, ws, ws_bytes, labels, acc, mode,
-                        stream, "dkm_partial_sum_f64");
+  return assign<double>(X, n, d, ldx, C, k, ws, ws_bytes, labels, acc, 1,
+                        mode, stream, "dkm_partial_sum_f64");
 }
 
 int dkm_partial_sum_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
@@ -777,15 +849,35 @@ int dkm_partial_sum_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
                         size_t ws_bytes, int32_t *labels, double *acc,
                         int mode, void *stream) {
   if (!acc) return fail(DKM_E_ARG, "partial_sum: acc is NULL");
-  return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, acc, mode,
-                       stream, "dkm_partial_sum_f32");
+  return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, acc, 1,
+                       mode, stream, "dkm_partial_sum_f32");
+}
+
+int dkm_assign_delta_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
+                         const double *C, int64_t k, const void *ws,
+                         size_t ws_bytes, int32_t *labels, double *delta,
+                         int mode, void *stream) {
+  if (!labels || !delta)
+    return fail(DKM_E_ARG, "assign_delta: labels and delta are required");
+  return assign<double>(X, n, d, ldx, C, k, ws, ws_bytes, labels, delta, 2,
+                        mode, stream, "dkm_assign_delta_f64");
+}
+
+int dkm_assign_delta_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
+                         const double *C, int64_t k, const void *ws,
+                         size_t ws_bytes, int32_t *labels, double *delta,
+                         int mode, void *stream) {
+  if (!labels || !delta)
+    return fail(DKM_E_ARG, "assign_delta: labels and delta are required");
+  return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, delta, 2,
+                       mode, stream, "dkm_assign_delta_f32");
 }
 
 int dkm_predict_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
                     const double *C, int64_t k, const void *ws,
                     size_t ws_bytes, int32_t *labels, int mode, void *stream) {
   if (!labels) return fail(DKM_E_ARG, "predict: labels is NULL");
-  return assign<double>(X, n, d, ldx, C, k, ws, ws_bytes, labels, nullptr,
+  return assign<double>(X, n, d, ldx, C, k, ws, ws_bytes, labels, nullptr, 0,
                         mode, stream, "dkm_predict_f64");
 }
 
@@ -793,8 +885,16 @@ int dkm_predict_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
                     const double *C, int64_t k, const void *ws,
                     size_t ws_bytes, int32_t *labels, int mode, void *stream) {
   if (!labels) return fail(DKM_E_ARG, "predict: labels is NULL");
-  return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, nullptr,
+  return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, nullptr, 0,
                        mode, stream, "dkm_predict_f32");
+}
+
+int dkm_add_f64(double *y, const double *x, int64_t n, void *stream) {
+  if ((!y || !x) && n > 0) return fail(DKM_E_ARG, "add: NULL");
+  if (n <= 0) return 0;
+  const int64_t g = std::min<int64_t>((n + 255) / 256, 4096);
+  k_add<<<(unsigned)g, 256, 0, (hipStream_t)stream>>>(y, x, n);
+  return check_launch("dkm_add_f64");
 }
 
 }  // extern "C"

@@ -87,6 +87,26 @@ int dkm_partial_sum_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
                         size_t ws_bytes, int32_t *labels, double *acc,
                         int mode, void *stream);
 
+/* Incremental form of dkm_partial_sum for the Lloyd loop.  labels (int32[n],
+ * in/out) holds each sample's previous label (-1 = none); on return it holds
+ * the new labels (identical to dkm_partial_sum's) and delta (k*(d+1), +=)
+ * has received +x / +1 for every sample that joined a cluster and -x / -1
+ * for every sample that left one, so acc_new = acc_old + delta is the
+ * [sums | counts] of the new assignment (up to fp64 rounding order).  After
+ * the first iterations few labels change, so almost no sample is added
+ * anywhere; the caller refreshes acc from scratch periodically.           */
+int dkm_assign_delta_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
+                         const double *C, int64_t k, const void *ws,
+                         size_t ws_bytes, int32_t *labels, double *delta,
+                         int mode, void *stream);
+int dkm_assign_delta_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
+                         const double *C, int64_t k, const void *ws,
+                         size_t ws_bytes, int32_t *labels, double *delta,
+                         int mode, void *stream);
+
+/* y[i] += x[i] (device, fp64): acc_new = acc_old + delta.                  */
+int dkm_add_f64(double *y, const double *x, int64_t n, void *stream);
+
 /* Assignment only.  Replaces `_predict` (base.py:194-201).  Needs a prepared
  * workspace (dkm_prepare_centers with acc = NULL is allowed).             */
 int dkm_predict_f64(const double *X, int64_t n, int64_t d, int64_t ldx,

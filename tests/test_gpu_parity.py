@@ -363,3 +363,71 @@ def test_large_fit_properties():
     rl, rs, rc = orc.partial_sum(X[:300000].cpu().numpy(), C)
     assert np.array_equal(labs, rl)
     _close(sums, rs, 1e-11)
+
+
+# ---------------------------------------------------------------------------
+# incremental (delta) assignment used by the fit loop
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("d,k", [(32, 100), (7, 5), (64, 40)])
+def test_assign_delta_equals_difference_of_partial_sums(mode, d, k):
+    from dislib_amd import _device, _lib
+    rng = np.random.default_rng(d * 100 + k)
+    n = 20000
+    x = rng.standard_normal((n, d)) * 4 + rng.uniform(-3, 3, (1, d))
+    C = x[rng.choice(n, k, replace=False)].copy()
+    prev = rng.integers(-1, k, n).astype(np.int32)
+    dev = torch.device("cuda")
+    ds = _load(x, n)
+    dd = ds._device_data()
+    Ct = torch.from_numpy(C).to(dev)
+    ws = _device.Workspace(k, d, n, dev)
+    acc = torch.zeros(k * (d + 1), dtype=torch.float64, device=dev)
+    lab = torch.from_numpy(prev.copy()).to(dev)
+    m = {"exact": _lib.MODE_EXACT, "screen32": _lib.MODE_SCREEN32,
+         "bf16x3": _lib.MODE_BF16X3}[mode]
+    _device.prepare(Ct, ws, acc)
+    _device.assign_delta(dd, Ct, ws, lab, acc, m)
+    new = lab.cpu().numpy()
+    rl, rs, rc = orc.partial_sum(x, C)
+    assert np.array_equal(new, rl)
+    # expected delta: sums(new) - sums(prev labels >= 0)
+    ps = np.zeros((k, d))
+    pc = np.zeros(k)
+    ok = prev >= 0
+    np.add.at(ps, prev[ok], x[ok])
+    np.add.at(pc, prev[ok], 1)
+    a = acc.cpu().numpy()
+    _close(a[:k * d].reshape(k, d), rs - ps, 1e-11)
+    assert np.array_equal(a[k * d:], rc - pc)
+
+
+@pytest.mark.parametrize("refresh", [1, 3, 1000])
+def test_fit_delta_refresh_matches_oracle(refresh):
+    import dislib_amd.cluster.kmeans as km_mod
+    g = load_golden("f05_c2mini")
+    x, _ = make_blobs(n_samples=20000, n_features=32, centers=100,
+                      center_box=(-10, 10), random_state=1)
+    old = km_mod.REFRESH
+    km_mod.REFRESH = refresh
+    try:
+        ds = _load(x, 5000)
+        km = _km(n_clusters=100, max_iter=3, tol=0, random_state=0)
+        km.fit_predict(ds)
+    finally:
+        km_mod.REFRESH = old
+    assert np.array_equal(_labels(ds), g["labels"])
+    _close(km.centers, g["centers"], RTOL64)
+    # longer run: refresh vs no refresh agree
+    ref = orc.OracleKMeans(n_clusters=20, max_iter=15, tol=0, random_state=5)
+    rl = ref.fit([x[i:i + 5000] for i in range(0, 20000, 5000)],
+                 set_labels=True)
+    km_mod.REFRESH = refresh
+    try:
+        ds = _load(x, 5000)
+        km = _km(n_clusters=20, max_iter=15, tol=0, random_state=5)
+        km.fit_predict(ds)
+    finally:
+        km_mod.REFRESH = old
+    assert np.array_equal(_labels(ds), rl)
+    _close(km.centers, ref.centers, RTOL64)
