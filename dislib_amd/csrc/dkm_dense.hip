@@ -384,8 +384,14 @@ __global__ void __launch_bounds__(SB)
       b2[b] = INFINITY;
       i1[b] = 0;
     }
-    for (int cb = 0; cb < nkb; ++cb) {
-      f32x4 accv[NB];
+    // MFMA chain of centre block cb into acc[]; consumed one chain later:
+    // the chain of block cb+1 is issued before block cb's accumulators are
+    // read, which keeps >= 6 MFMAs between an MFMA and the first VALU read
+    // of its result.  (ROCm 7.2's hazard model under-counts the wait states
+    // before v_accvgpr_read of a v_mfma_f32_16x16x32_bf16 result on gfx950:
+    // with the compiler's spacing, about 1e-5 of the labels came out wrong
+    // at random -- tools/debug_mismatch.py.)
+    auto chain = [&](int cb, f32x4 (&accv)[NB]) {
 #pragma unroll
       for (int b = 0; b < NB; ++b) accv[b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -418,6 +424,8 @@ __global__ void __launch_bounds__(SB)
                                                               accv[b], 0, 0, 0);
         }
       }
+    };
+    auto score = [&](int cb, const f32x4 (&accv)[NB]) {
       const float4 cn4 = *(const float4 *)(cn + cb * 16 + 4 * q);
       const float cnv[4] = {cn4.x, cn4.y, cn4.z, cn4.w};
       const int cbase = cb * 16 + 4 * q;
@@ -442,6 +450,28 @@ __global__ void __launch_bounds__(SB)
           b1[b] = fminf(b1[b], sc[b]);
         }
       }
+    };
+    f32x4 acc_a[NB], acc_b[NB];
+    chain(0, acc_a);
+    int cb = 0;
+    for (; cb + 2 <= nkb; cb += 2) {  // ping-pong: no runtime-indexed arrays
+      chain(cb + 1, acc_b);
+      __builtin_amdgcn_sched_barrier(0);
+      score(cb, acc_a);
+      if (cb + 2 < nkb) chain(cb + 2, acc_a);
+      __builtin_amdgcn_sched_barrier(0);
+      if (cb + 2 >= nkb) {
+        // last chain: no MFMAs left to cover its latency
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      score(cb + 1, acc_b);
+    }
+    if (cb < nkb) {  // odd block count: acc_a holds the final chain
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      score(cb, acc_a);
     }
     // merge the top-2 of the four lanes of a sample (first index on ties)
 #pragma unroll

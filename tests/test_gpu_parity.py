@@ -431,3 +431,38 @@ def test_fit_delta_refresh_matches_oracle(refresh):
         km_mod.REFRESH = old
     assert np.array_equal(_labels(ds), rl)
     _close(km.centers, ref.centers, RTOL64)
+
+
+@pytest.mark.parametrize("mode", ["screen32", "bf16x3"])
+def test_screen_stress_vs_exact_kernel(mode):
+    """1M samples x 2 repetitions against the exact kernel on the same
+    (fitted) centres: a timing hazard or race that corrupts a handful of
+    labels per million shows up here (the exact kernel itself is pinned to
+    the oracle by the tests above)."""
+    from dislib_amd import _device, _lib
+    from dislib_amd.data import Dataset, Subset
+    n, d, k = 1_000_000, 32, 100
+    X = torch.empty((n, d), dtype=torch.float64, device="cuda")
+    _device.make_blobs(X, 0, k, seed=3)
+    ds = Dataset(n_features=d)
+    ds.append(Subset(X))
+    km = _km(n_clusters=k, max_iter=3, tol=0, random_state=0)
+    km.fit(ds)
+    dd = ds._device_data()
+    C = torch.from_numpy(km.centers).to("cuda")
+    ws = _device.Workspace(k, d, n, torch.device("cuda"))
+    acc = torch.zeros(k * (d + 1), dtype=torch.float64, device="cuda")
+    ref = torch.empty(n, dtype=torch.int32, device="cuda")
+    _device.prepare(C, ws, acc)
+    _device.predict(dd, C, ws, ref, _lib.MODE_EXACT)
+    m = {"screen32": _lib.MODE_SCREEN32, "bf16x3": _lib.MODE_BF16X3}[mode]
+    for rep in range(2):
+        lab = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+        _device.prepare(C, ws, acc)
+        _device.partial_sum(dd, C, ws, lab, acc, m)
+        bad = int((lab != ref).sum().item())
+        assert bad == 0, "%d labels differ (rep %d)" % (bad, rep)
+        lab.fill_(-7)
+        _device.predict(dd, C, ws, lab, m)
+        bad = int((lab != ref).sum().item())
+        assert bad == 0, "%d predict labels differ (rep %d)" % (bad, rep)
