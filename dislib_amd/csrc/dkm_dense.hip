@@ -384,13 +384,13 @@ __global__ void __launch_bounds__(SB)
       b2[b] = INFINITY;
       i1[b] = 0;
     }
-    // MFMA chain of centre block cb into acc[]; consumed one chain later:
-    // the chain of block cb+1 is issued before block cb's accumulators are
-    // read, which keeps >= 6 MFMAs between an MFMA and the first VALU read
-    // of its result.  (ROCm 7.2's hazard model under-counts the wait states
-    // before v_accvgpr_read of a v_mfma_f32_16x16x32_bf16 result on gfx950:
-    // with the compiler's spacing, about 1e-5 of the labels came out wrong
-    // at random -- tools/debug_mismatch.py.)
+    // MFMA chain of centre block cb into acc[], consumed one chain later,
+    // and every chain is followed by a drain fence of 24 wait states before
+    // any VALU/DS instruction may touch its operands or results.  ROCm 7.2's
+    // hazard model under-counts the latency of v_mfma_f32_16x16x32_bf16 on
+    // gfx950: with the compiler's own spacing about 1e-5 of the labels came
+    // out wrong at random (tools/debug_mismatch.py; a fence after each chain
+    // removed every error, pipelining alone did not).
     auto chain = [&](int cb, f32x4 (&accv)[NB]) {
 #pragma unroll
       for (int b = 0; b < NB; ++b) accv[b] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -451,28 +451,26 @@ __global__ void __launch_bounds__(SB)
         }
       }
     };
-    f32x4 acc_a[NB], acc_b[NB];
-    chain(0, acc_a);
-    int cb = 0;
-    for (; cb + 2 <= nkb; cb += 2) {  // ping-pong: no runtime-indexed arrays
-      chain(cb + 1, acc_b);
-      __builtin_amdgcn_sched_barrier(0);
-      score(cb, acc_a);
-      if (cb + 2 < nkb) chain(cb + 2, acc_a);
-      __builtin_amdgcn_sched_barrier(0);
-      if (cb + 2 >= nkb) {
-        // last chain: no MFMAs left to cover its latency
-        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      score(cb + 1, acc_b);
-    }
-    if (cb < nkb) {  // odd block count: acc_a holds the final chain
+    auto drain = [&]() {
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+    };
+    f32x4 acc_a[NB], acc_b[NB];
+    chain(0, acc_a);
+    drain();
+    int cb = 0;
+    for (; cb + 2 <= nkb; cb += 2) {  // ping-pong: no runtime-indexed arrays
+      chain(cb + 1, acc_b);
+      drain();
       score(cb, acc_a);
+      if (cb + 2 < nkb) {
+        chain(cb + 2, acc_a);
+        drain();
+      }
+      score(cb + 1, acc_b);
     }
+    if (cb < nkb) score(cb, acc_a);  // odd block count: final chain in acc_a
     // merge the top-2 of the four lanes of a sample (first index on ties)
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
