@@ -20,6 +20,13 @@
 //   k_recheck_scan     exact arithmetic for the undecided samples (wave per
 //                      sample, lanes over centres, coalesced C^T reads).
 //
+// Toolchain note (ROCm 7.2, gfx950): no packed-fp32 VALU (v_pk_fma_f32 and
+// friends) in these kernels.  hipcc reused a source VGPR of a v_pk_fma_f32
+// as the destination of a VALU op three instructions later, and lanes 48-63
+// of the packed op read the clobbered value: ~1e-5 of the labels went wrong
+// at random (tools/debug_mismatch.py pinned it to MFMA row 13 = lanes 48-63,
+// element 1).  Scalar fmaf + -fno-slp-vectorize; tests check the ISA.
+//
 // Accumulation (acc = [sums k*d | counts k], fp64):
 //   AM_LDS / AM_GLOBAL  every sample adds its row (partial_sum semantics);
 //                       LDS-private accumulators (odd row stride) flushed
@@ -384,13 +391,8 @@ __global__ void __launch_bounds__(SB)
       b2[b] = INFINITY;
       i1[b] = 0;
     }
-    // MFMA chain of centre block cb into acc[], consumed one chain later,
-    // and every chain is followed by a drain fence of 24 wait states before
-    // any VALU/DS instruction may touch its operands or results.  ROCm 7.2's
-    // hazard model under-counts the latency of v_mfma_f32_16x16x32_bf16 on
-    // gfx950: with the compiler's own spacing about 1e-5 of the labels came
-    // out wrong at random (tools/debug_mismatch.py; a fence after each chain
-    // removed every error, pipelining alone did not).
+    // MFMA chain of centre block cb into acc[]; consumed one chain later so
+    // that the next block's MFMAs overlap this block's VALU scoring.
     auto chain = [&](int cb, f32x4 (&accv)[NB]) {
 #pragma unroll
       for (int b = 0; b < NB; ++b) accv[b] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -431,17 +433,11 @@ __global__ void __launch_bounds__(SB)
       const int cbase = cb * 16 + 4 * q;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        // scalar fmaf on purpose: no v_pk_*_f32 anywhere (see the header
+        // note on packed-VALU operand hazards; built -fno-slp-vectorize)
         float sc[NB];
-        if constexpr (NB == 2) {
-          const f32x2 s2 = __builtin_elementwise_fma(
-              f32x2{accv[0][i], accv[1][i]}, f32x2{-2.f, -2.f},
-              f32x2{cnv[i], cnv[i]});
-          sc[0] = s2.x;
-          sc[1] = s2.y;
-        } else {
 #pragma unroll
-          for (int b = 0; b < NB; ++b) sc[b] = fmaf(-2.f, accv[b][i], cnv[i]);
-        }
+        for (int b = 0; b < NB; ++b) sc[b] = fmaf(-2.f, accv[b][i], cnv[i]);
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
           // b1 <= b2: new second = med3(b1, b2, s); ties -> b2 == b1
@@ -451,23 +447,13 @@ __global__ void __launch_bounds__(SB)
         }
       }
     };
-    auto drain = [&]() {
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    };
     f32x4 acc_a[NB], acc_b[NB];
     chain(0, acc_a);
-    drain();
     int cb = 0;
     for (; cb + 2 <= nkb; cb += 2) {  // ping-pong: no runtime-indexed arrays
       chain(cb + 1, acc_b);
-      drain();
       score(cb, acc_a);
-      if (cb + 2 < nkb) {
-        chain(cb + 2, acc_a);
-        drain();
-      }
+      if (cb + 2 < nkb) chain(cb + 2, acc_a);
       score(cb + 1, acc_b);
     }
     if (cb < nkb) score(cb, acc_a);  // odd block count: final chain in acc_a

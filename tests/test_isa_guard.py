@@ -1,0 +1,40 @@
+"""CPU guard on the generated gfx950 ISA (compiles the kernels to device
+assembly with the Makefile's flags; no GPU needed).
+
+ROCm 7.2 hipcc on gfx950 produced a packed-fp32 (v_pk_fma_f32) operand
+hazard in the screen kernel: lanes 48-63 read a source VGPR already
+overwritten by a later VALU op.  The kernels
+therefore must contain no v_pk_*_f32 instruction.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "dislib_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+def _flags():
+    mk = open(os.path.join(CSRC, "Makefile")).read()
+    m = re.search(r"^FLAGS\s*:=\s*(.*?)(?<!\\)\n", mk, re.S | re.M)
+    flags = m.group(1).replace("\\\n", " ").replace("$(ARCH)", "gfx950")
+    return [f for f in flags.split() if f not in ("-fPIC",)]
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not present")
+@pytest.mark.parametrize("src", ["dkm_dense.hip", "dkm_util.hip",
+                                 "dkm_sparse.hip"])
+def test_no_packed_fp32_valu(src, tmp_path):
+    out = tmp_path / (src + ".s")
+    cmd = [HIPCC] + _flags() + ["-S", "--cuda-device-only",
+                                os.path.join(CSRC, src), "-o", str(out)]
+    subprocess.check_call(cmd, cwd=CSRC, stdout=subprocess.DEVNULL,
+                          stderr=subprocess.DEVNULL)
+    asm = out.read_text()
+    bad = sorted(set(re.findall(r"\bv_pk_\w*f32\b", asm)))
+    assert not bad, "packed fp32 VALU in %s: %s" % (src, bad)
+    assert "-fno-slp-vectorize" in _flags()
