@@ -16,9 +16,11 @@
 //   k_screen           MFMA screen: s_j = |c_j|^2 - 2 x.c_j (fp32 or bf16x3
 //                      split precision), a rigorous error bound decides
 //                      whether the screened winner IS the reference winner;
-//                      otherwise the label is left for ...
-//   k_recheck_scan     exact arithmetic for the undecided samples (wave per
-//                      sample, lanes over centres, coalesced C^T reads).
+//                      otherwise the label is left for the re-check.
+//   k_recheck_lane     undecided samples, compacted per wave, lane per
+//                      sample: fp32 re-screen, then the reference
+//                      arithmetic on the remaining candidate centres.
+//   k_recheck_exact    the reference arithmetic on all centres (any d, k).
 //
 // Toolchain note (ROCm 7.2, gfx950): no packed-fp32 VALU (v_pk_fma_f32 and
 // friends) in these kernels.  hipcc reused a source VGPR of a v_pk_fma_f32
@@ -28,12 +30,14 @@
 // element 1).  Scalar fmaf + -fno-slp-vectorize; tests check the ISA.
 //
 // Accumulation (acc = [sums k*d | counts k], fp64):
-//   AM_LDS / AM_GLOBAL  every sample adds its row (partial_sum semantics);
-//                       LDS-private accumulators (odd row stride) flushed
-//                       once per block, or fp64 global atomics.
-//   AM_DELTA            incremental: labels[] holds the previous assignment;
-//                       only samples whose label changes add +x to the new
-//                       and -x to the old cluster (dkm_assign_delta).
+//   full   every sample adds its row (partial_sum semantics);
+//   delta  incremental: labels[] holds the previous assignment; only samples
+//          whose label changes add +x to the new and -x to the old cluster
+//          (dkm_assign_delta).
+// Both go to block-private LDS accumulators (odd row stride, flushed once
+// per block) when they fit, else to fp64 global atomics.  Delta in LDS
+// matters: in the first iterations most labels move, and global atomics on
+// k rows serialise (a 100M x 32, k = 100 delta pass took 650 ms that way).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -47,7 +51,13 @@ namespace dkm {
 constexpr int BLOCK = 256;
 constexpr size_t LDS_BUDGET = 80 * 1024;  // per block -> >= 2 blocks / CU
 
-enum AccMode { AM_NONE = 0, AM_LDS = 1, AM_GLOBAL = 2, AM_DELTA = 3 };
+// Accumulation mode bits: AM_ON (accumulate at all), AM_DELTA (incremental:
+// only label changes move rows), AM_INLDS (block-private LDS accumulators,
+// flushed once per block; else fp64 global atomics).
+enum : int { AM_NONE = 0, AM_ON = 1, AM_DELTA = 2, AM_INLDS = 4 };
+__host__ __device__ __forceinline__ bool am_full(int m) {
+  return (m & (AM_ON | AM_DELTA)) == AM_ON;
+}
 
 struct DevInfo {
   int cus = 256;
@@ -86,31 +96,54 @@ __device__ __forceinline__ void lds_add(double *p, double v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Accumulate one sample (lane-per-sample kernels).
-template <class TX>
-__device__ __forceinline__ void acc_row_lane(int amode, double *lds_acc,
-                                             double *acc, int64_t k, int d,
-                                             int label, int prev,
-                                             const TX *xrow) {
-  if (amode == AM_LDS) {
-    const int ds = lds_stride(d);
-    double *srow = lds_acc + (int64_t)label * ds;
-    for (int t = 0; t < d; ++t) lds_add(srow + t, ld_x(xrow + t));
-    lds_add(lds_acc + k * ds + label, 1.0);
-  } else if (amode == AM_GLOBAL) {
-    double *srow = acc + (int64_t)label * d;
-    for (int t = 0; t < d; ++t) atomic_add_f64(srow + t, ld_x(xrow + t));
-    atomic_add_f64(acc + k * d + label, 1.0);
-  } else if (amode == AM_DELTA && label != prev) {
-    double *srow = acc + (int64_t)label * d;
-    for (int t = 0; t < d; ++t) atomic_add_f64(srow + t, ld_x(xrow + t));
-    atomic_add_f64(acc + k * d + label, 1.0);
-    if (prev >= 0) {
-      double *orow = acc + (int64_t)prev * d;
-      for (int t = 0; t < d; ++t) atomic_add_f64(orow + t, -ld_x(xrow + t));
-      atomic_add_f64(acc + k * d + prev, -1.0);
-    }
+// Where one kernel's sums go: LDS rows (odd stride) or the global acc.
+struct AccTarget {
+  double *rows;
+  double *cnt;
+  int stride;
+  bool lds;
+  __device__ __forceinline__ void add(int row, int t, double v) const {
+    double *p = rows + (int64_t)row * stride + t;
+    if (lds)
+      lds_add(p, v);
+    else
+      atomic_add_f64(p, v);
   }
+  __device__ __forceinline__ void count(int row, double v) const {
+    if (lds)
+      lds_add(cnt + row, v);
+    else
+      atomic_add_f64(cnt + row, v);
+  }
+};
+
+__device__ __forceinline__ AccTarget acc_target(int amode, double *lds_acc,
+                                                double *acc, int64_t k,
+                                                int d) {
+  if (amode & AM_INLDS) {
+    const int ds = lds_stride(d);
+    return AccTarget{lds_acc, lds_acc + k * ds, ds, true};
+  }
+  return AccTarget{acc, acc + k * d, d, false};
+}
+
+// Accumulate one sample (lane-per-sample kernels): +x to `label`, and in
+// delta mode (only when the label changed) -x from `prev`.
+template <class TX>
+__device__ __forceinline__ void acc_row_lane(int amode, const AccTarget &a,
+                                             int d, int label, int prev,
+                                             const TX *xrow) {
+  if (!(amode & AM_ON)) return;
+  const bool delta = amode & AM_DELTA;
+  if (delta && label == prev) return;
+  const bool sub = delta && prev >= 0;
+  for (int t = 0; t < d; ++t) {
+    const double x = ld_x(xrow + t);
+    a.add(label, t, x);
+    if (sub) a.add(prev, t, -x);
+  }
+  a.count(label, 1.0);
+  if (sub) a.count(prev, -1.0);
 }
 
 __device__ __forceinline__ void zero_lds_acc(double *lds_acc, int64_t k,
@@ -140,11 +173,12 @@ __global__ void __launch_bounds__(BLOCK)
                 double *acc, int amode) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double *cl = smem;                         // k*d centres
-  double *lds_acc = smem + (int64_t)k * d;   // accumulators (AM_LDS)
+  double *lds_acc = smem + (int64_t)k * d;   // accumulators (AM_INLDS)
   const int64_t kd = (int64_t)k * d;
   for (int64_t e = threadIdx.x; e < kd; e += blockDim.x) cl[e] = C[e];
-  if (amode == AM_LDS) zero_lds_acc(lds_acc, k, d);
+  if (amode & AM_INLDS) zero_lds_acc(lds_acc, k, d);
   __syncthreads();
+  const AccTarget at = acc_target(amode, lds_acc, acc, k, d);
 
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -169,11 +203,11 @@ __global__ void __launch_bounds__(BLOCK)
         best_s = s;
       }
     }
-    const int prev = (amode == AM_DELTA) ? labels[i] : -1;
+    const int prev = (amode & AM_DELTA) ? labels[i] : -1;
     if (labels) labels[i] = bi;
-    acc_row_lane(amode, lds_acc, acc, k, d, bi, prev, xr);
+    acc_row_lane(amode, at, d, bi, prev, xr);
   }
-  if (amode == AM_LDS) {
+  if (amode & AM_INLDS) {
     __syncthreads();
     flush_lds_acc(lds_acc, acc, k, d);
   }
@@ -209,20 +243,21 @@ __global__ void __launch_bounds__(BLOCK)
                 double *acc, int amode) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double *lds_acc = smem;
-  if (amode == AM_LDS) {
+  if (amode & AM_INLDS) {
     zero_lds_acc(lds_acc, k, d);
     __syncthreads();
   }
+  const AccTarget at = acc_target(amode, lds_acc, acc, k, d);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += stride) {
     const TX *xr = X + i * ldx;
     const int bi = exact_label_lane(xr, d, C, k);
-    const int prev = (amode == AM_DELTA) ? labels[i] : -1;
+    const int prev = (amode & AM_DELTA) ? labels[i] : -1;
     if (labels) labels[i] = bi;
-    acc_row_lane(amode, lds_acc, acc, k, d, bi, prev, xr);
+    acc_row_lane(amode, at, d, bi, prev, xr);
   }
-  if (amode == AM_LDS) {
+  if (amode & AM_INLDS) {
     __syncthreads();
     flush_lds_acc(lds_acc, acc, k, d);
   }
@@ -307,8 +342,8 @@ __device__ __forceinline__ void load8(const TX *xr, int t0, int d,
 // the dots of centres cb*16 + 4q + i (i < 4) with sample j; each lane keeps a
 // top-2 (fma, cmp, cndmask, med3, min per score), two xor-shuffles merge the
 // four lanes of a sample.  lab_out[si] = label, or -(prev + 2) when the
-// screen cannot decide (k_recheck_scan computes it exactly; prev = -1
-// outside AM_DELTA).
+// screen cannot decide (the re-check resolves it; prev = -1 outside
+// AM_DELTA).
 template <int PREC, int NKS, int NB, bool VEC, class TX>
 __global__ void __launch_bounds__(SB)
     k_screen(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
@@ -327,12 +362,13 @@ __global__ void __launch_bounds__(SB)
     f32x4 *dst = (f32x4 *)frag;
     for (int e = threadIdx.x; e < nkb * NKS * 128; e += SB) dst[e] = src[e];
     for (int e = threadIdx.x; e < nkb * 16; e += SB) cn[e] = v.cnpad[e];
-    if (amode == AM_LDS) zero_lds_acc(lds_acc, k, d);
+    if (amode & AM_INLDS) zero_lds_acc(lds_acc, k, d);
   }
   const float cm =
       (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
-  const int ds = lds_stride(d);
-  const bool full_acc = (amode == AM_LDS || amode == AM_GLOBAL);
+  const bool full_acc = am_full(amode);
+  const bool delta = amode & AM_DELTA;
+  const AccTarget at = acc_target(amode, lds_acc, acc, k, d);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
@@ -481,34 +517,21 @@ __global__ void __launch_bounds__(SB)
       const bool unique = sane && (b2[b] - b1[b] > 2.0f * B);
       const int lab = i1[b];
       int prev = -1;
-      if (amode == AM_DELTA) prev = lab_out[si];  // 16 lanes x 4 B, coalesced
+      if (delta) prev = lab_out[si];  // 16 lanes x 4 B, coalesced
       if (q == 0) lab_out[si] = unique ? lab : -(prev + 2);
-      if (!unique) continue;  // label + sums by k_recheck_scan
-      if (amode == AM_LDS) {
-        double *srow = lds_acc + (int64_t)lab * ds;
+      if (!unique) continue;  // label + sums by the re-check
+      if (full_acc) {
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
           for (int m = 0; m < 8; ++m) {
             const int t = ks * 32 + 8 * q + m;
-            if (t < d) lds_add(srow + t, tile[b][ks][m]);
+            if (t < d) at.add(lab, t, tile[b][ks][m]);
           }
-        if (q == 0) lds_add(lds_acc + (int64_t)k * ds + lab, 1.0);
-      } else if (amode == AM_GLOBAL) {
-        double *srow = acc + (int64_t)lab * d;
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-          for (int m = 0; m < 8; ++m) {
-            const int t = ks * 32 + 8 * q + m;
-            if (t < d) atomic_add_f64(srow + t, tile[b][ks][m]);
-          }
-        if (q == 0) atomic_add_f64(acc + (int64_t)k * d + lab, 1.0);
-      } else if (amode == AM_DELTA && lab != prev) {
+        if (q == 0) at.count(lab, 1.0);
+      } else if (delta && lab != prev) {
         // rare after the first iterations: reload the row (L2) and move it
         const TX *xr = X + si * ldx;
-        double *nrow = acc + (int64_t)lab * d;
-        double *orow = acc + (int64_t)(prev < 0 ? 0 : prev) * d;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
@@ -516,41 +539,255 @@ __global__ void __launch_bounds__(SB)
             const int t = ks * 32 + 8 * q + m;
             if (t < d) {
               const double x = ld_x(xr + t);
-              atomic_add_f64(nrow + t, x);
-              if (prev >= 0) atomic_add_f64(orow + t, -x);
+              at.add(lab, t, x);
+              if (prev >= 0) at.add(prev, t, -x);
             }
           }
         if (q == 0) {
-          atomic_add_f64(acc + (int64_t)k * d + lab, 1.0);
-          if (prev >= 0) atomic_add_f64(acc + (int64_t)k * d + prev, -1.0);
+          at.count(lab, 1.0);
+          if (prev >= 0) at.count(prev, -1.0);
         }
       }
     }
     if (full_acc && s_next < n) load_tile(s_next);  // the tile was in use
   }
-  if (amode == AM_LDS) {
+  if (amode & AM_INLDS) {
     __syncthreads();
     flush_lds_acc(lds_acc, acc, k, d);
   }
 }
 
 // Exact re-check of the samples the screen left undecided (lab_out < 0,
-// encoding the previous label as -(prev + 2)): each wave scans 64 labels at
-// a time (coalesced), and for every undecided one computes the reference
-// distance to all centres (lanes over centres, C^T reads coalesced), the
-// (dist, index) argmin, the label and the sums.  No shared counter.
-template <bool SMALL, class TX>
+// encoding the previous label as -(prev + 2)).  Waves scan 64 labels at a
+// time (coalesced, no shared counter).
+//   k_recheck_lane (d <= 128, fp32 centres fit in LDS): each wave compacts
+//     its undecided samples into an LDS list and resolves them 64 at a time,
+//     lane = sample.  Stage 1 re-screens in fp32 VALU (x in VGPRs, centres
+//     broadcast from LDS) -- the P_F32 arithmetic and bound, ~2^-24 instead
+//     of bf16x3's ~2^-16 -- and keeps the label when the best two scores are
+//     2B apart.  Otherwise stage 2 runs the reference arithmetic on the
+//     candidates only (score <= best + 2B: the reference winner is always
+//     among them, and every other centre is strictly farther after sqrt,
+//     DESIGN.md 3.1).
+//   k_recheck_exact (any d, k): wave per sample, lanes over centres, the
+//     reference arithmetic on every centre.
+template <class TX>
+__device__ __forceinline__ void recheck_accumulate(int amode,
+                                                   const AccTarget &at,
+                                                   const TX *xr, int d,
+                                                   int bi, int prev,
+                                                   int lane) {
+  if (!(amode & AM_ON)) return;
+  const bool delta = amode & AM_DELTA;
+  if (delta && bi == prev) return;
+  const bool sub = delta && prev >= 0;
+  for (int t = lane; t < d; t += 64) {
+    const double x = ld_x(xr + t);
+    at.add(bi, t, x);
+    if (sub) at.add(prev, t, -x);
+  }
+  if (lane == 0) {
+    at.count(bi, 1.0);
+    if (sub) at.count(prev, -1.0);
+  }
+}
+
+__device__ __forceinline__ void recheck_finish_count(
+    unsigned long long mine, unsigned long long *blk_count, const WsView &v) {
+  if ((threadIdx.x & 63) == 0 && mine)
+    __hip_atomic_fetch_add(blk_count, mine, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();
+  if (threadIdx.x == 0 && *blk_count)
+    atomicAdd((unsigned long long *)&v.hdr->rechecked_total, *blk_count);
+}
+
+constexpr int RL_CAP = 128;  // per-wave list: a full batch + one chunk
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+static size_t recheck_lane_lds(int64_t k, int64_t d) {
+  const int64_t dp = round_up(d, 4);
+  return (size_t)round_up((k * dp + k) * 4, 8) +
+         (size_t)(BLOCK / 64) * RL_CAP * 8;
+}
+
+template <int MAXD, bool VEC, class TX>
 __global__ void __launch_bounds__(BLOCK)
-    k_recheck_scan(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
+    k_recheck_lane(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
                    int k, WsView v, int32_t *__restrict__ lab_out,
                    double *acc, int amode, int64_t base) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int dp = (int)round_up(d, 4);  // c32 row stride (dkm_util)
+  float *cl = (float *)smem;           // fp32 centres, k x dp (zero padded)
+  float *cnl = cl + (int64_t)k * dp;   // |c|^2 fp32
+  int64_t *lists =
+      (int64_t *)((char *)smem + round_up(((int64_t)k * dp + k) * 4, 8));
+  double *lds_acc = (double *)(lists + (BLOCK / 64) * RL_CAP);
+  __shared__ unsigned long long blk_count;
+  if (threadIdx.x == 0) blk_count = 0;
+  {
+    const f32x4 *src = (const f32x4 *)v.c32;
+    f32x4 *dst = (f32x4 *)cl;
+    for (int64_t e = threadIdx.x; e < (int64_t)k * dp / 4; e += BLOCK)
+      dst[e] = src[e];
+    for (int e = threadIdx.x; e < k; e += BLOCK) cnl[e] = v.cn32[e];
+  }
+  if (amode & AM_INLDS) zero_lds_acc(lds_acc, k, d);
+  const float cm =
+      (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
+  const AccTarget at = acc_target(amode, lds_acc, acc, k, d);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  int64_t *wl = lists + (threadIdx.x >> 6) * RL_CAP;
+
+  // one undecided sample per lane
+  auto resolve = [&](int64_t i) {
+    const int prev = -lab_out[i] - 2;
+    const TX *xr = X + i * ldx;
+    float xf[MAXD];
+    float xx = 0.f;
+#pragma unroll
+    for (int b = 0; b < MAXD / 8; ++b) {
+      double o[8];
+      if (8 * b < d) {
+        load8<VEC>(xr, 8 * b, d, o);
+      } else {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) o[m] = 0.0;
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        xf[8 * b + m] = (float)o[m];
+        xx = fmaf(xf[8 * b + m], xf[8 * b + m], xx);
+      }
+    }
+    // fp32 score of centre j: fma chain over features (padding adds 0 * 0)
+    auto score = [&](int j) {
+      const float *cr = cl + (int64_t)j * dp;
+      float dot = 0.f;
+#pragma unroll
+      for (int t4 = 0; t4 < MAXD / 4; ++t4) {
+        if (4 * t4 < dp) {
+          const f32x4 c4 = *(const f32x4 *)(cr + 4 * t4);
+          dot = fmaf(xf[4 * t4 + 0], c4.x, dot);
+          dot = fmaf(xf[4 * t4 + 1], c4.y, dot);
+          dot = fmaf(xf[4 * t4 + 2], c4.z, dot);
+          dot = fmaf(xf[4 * t4 + 3], c4.w, dot);
+        }
+      }
+      return fmaf(-2.f, dot, cnl[j]);
+    };
+    float b1 = INFINITY, b2 = INFINITY;
+    int i1 = 0;
+    for (int j = 0; j < k; ++j) {
+      const float sc = score(j);
+      i1 = sc < b1 ? j : i1;
+      b2 = __builtin_amdgcn_fmed3f(b1, b2, sc);
+      b1 = fminf(b1, sc);
+    }
+    const float xn = sqrtf(xx) * (1.0f + (d + 4) * 0x1.0p-24f);
+    const float B = screen_bound<P_F32>(d, xn, cm);
+    const bool sane = (xn < 1e18f) && (xn * cm < 1e30f) && (b1 < 1e30f);
+    int bi = i1;
+    if (!(sane && b2 - b1 > 2.0f * B)) {
+      const float lim = b1 + 2.0f * B;
+      double best = INFINITY;
+      bi = -1;
+      for (int j = 0; j < k; ++j) {
+        if (sane && !(score(j) <= lim)) continue;
+        const SqDiffT<TX> f{xr, v.ct64 + j, (int64_t)k};
+        const double dist = sqrt(pw_leaf(f, 0, d));
+        if (dist < best || bi < 0) {
+          best = dist;
+          bi = j;
+        }
+      }
+    }
+    lab_out[i] = bi;
+    if (!(amode & AM_ON)) return;
+    const bool delta = amode & AM_DELTA;
+    if (delta && bi == prev) return;
+    const bool sub = delta && prev >= 0;
+    for (int t = 0; t < d; ++t) {
+      const double x = ld_x(xr + t);
+      at.add(bi, t, x);
+      if (sub) at.add(prev, t, -x);
+    }
+    at.count(bi, 1.0);
+    if (sub) at.count(prev, -1.0);
+  };
+
+  // Scan: 4 labels per lane (int4), 256 per wave step, the next step's
+  // labels in flight while this one resolves (a wave's list only holds
+  // samples of steps it has already scanned, so the prefetch is never stale).
+  // a0 aligns the int4 loads; lanes outside [base, n) read nothing.
+  const int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+  const int64_t nwv = (int64_t)gridDim.x * (BLOCK / 64);
+  const int64_t a0 =
+      base - (int64_t)(((uintptr_t)(lab_out + base) >> 2) & 3);
+  auto load4 = [&](int64_t c0, int (&o)[4]) {
+    const int64_t i0 = c0 + 4 * lane;
+    if (i0 >= base && i0 + 3 < n) {
+      const int4 q4 = *(const int4 *)(lab_out + i0);
+      o[0] = q4.x; o[1] = q4.y; o[2] = q4.z; o[3] = q4.w;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        o[c] = (i0 + c >= base && i0 + c < n) ? lab_out[i0 + c] : 0;
+    }
+  };
+  unsigned long long mine = 0;
+  int cnt = 0;  // wave-uniform list length
+  int cur[4] = {0, 0, 0, 0};
+  int64_t c0 = a0 + wv * 256;
+  if (c0 < n) load4(c0, cur);
+  for (; c0 < n; c0 += nwv * 256) {
+    int nxt[4] = {0, 0, 0, 0};
+    if (c0 + nwv * 256 < n) load4(c0 + nwv * 256, nxt);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const unsigned long long mask = __ballot(cur[c] < 0);
+      if (cur[c] < 0)
+        wl[cnt + __popcll(mask & ((1ull << lane) - 1))] = c0 + 4 * lane + c;
+      const int add = __popcll(mask);
+      mine += add;
+      cnt += add;
+      if (cnt >= 64) {
+        wave_lds_sync();
+        resolve(wl[lane]);
+        const int rem = cnt - 64;
+        const int64_t tail = lane < rem ? wl[64 + lane] : 0;
+        wave_lds_sync();
+        if (lane < rem) wl[lane] = tail;
+        cnt = rem;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) cur[c] = nxt[c];
+  }
+  wave_lds_sync();
+  if (lane < cnt) resolve(wl[lane]);
+  recheck_finish_count(mine, &blk_count, v);
+  if (amode & AM_INLDS) flush_lds_acc(lds_acc, acc, k, d);
+}
+
+template <bool SMALL, class TX>
+__global__ void __launch_bounds__(BLOCK)
+    k_recheck_exact(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
+                    int k, WsView v, int32_t *__restrict__ lab_out,
+                    double *acc, int amode, int64_t base) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double *lds_acc = smem;
   __shared__ unsigned long long blk_count;
   if (threadIdx.x == 0) blk_count = 0;
-  if (amode == AM_LDS) zero_lds_acc(lds_acc, k, d);
+  if (amode & AM_INLDS) zero_lds_acc(lds_acc, k, d);
+  const AccTarget at = acc_target(amode, lds_acc, acc, k, d);
   __syncthreads();
-  const int ds = lds_stride(d);
   const int lane = threadIdx.x & 63;
   const int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
   const int64_t nwv = (int64_t)gridDim.x * (BLOCK / 64);
@@ -570,8 +807,7 @@ __global__ void __launch_bounds__(BLOCK)
       int bi = 0x7fffffff;  // lanes without a centre never win
       for (int jc = lane; jc < k; jc += 64) {
         const SqDiffT<TX> f{xr, v.ct64 + jc, (int64_t)k};
-        const double s2 = SMALL ? pw_leaf(f, 0, d) : pw_sum(f, d);
-        const double dist = sqrt(s2);
+        const double dist = sqrt(SMALL ? pw_leaf(f, 0, d) : pw_sum(f, d));
         if (dist < best || bi == 0x7fffffff) {
           best = dist;
           bi = jc;
@@ -579,32 +815,11 @@ __global__ void __launch_bounds__(BLOCK)
       }
       wave_argmin(best, bi);
       if (lane == 0) lab_out[i] = bi;
-      if (amode == AM_LDS) {
-        for (int t = lane; t < d; t += 64)
-          lds_add(lds_acc + (int64_t)bi * ds + t, ld_x(xr + t));
-        if (lane == 0) lds_add(lds_acc + (int64_t)k * ds + bi, 1.0);
-      } else if (amode == AM_GLOBAL || (amode == AM_DELTA && bi != prev)) {
-        for (int t = lane; t < d; t += 64) {
-          const double x = ld_x(xr + t);
-          atomic_add_f64(acc + (int64_t)bi * d + t, x);
-          if (amode == AM_DELTA && prev >= 0)
-            atomic_add_f64(acc + (int64_t)prev * d + t, -x);
-        }
-        if (lane == 0) {
-          atomic_add_f64(acc + (int64_t)k * d + bi, 1.0);
-          if (amode == AM_DELTA && prev >= 0)
-            atomic_add_f64(acc + (int64_t)k * d + prev, -1.0);
-        }
-      }
+      recheck_accumulate(amode, at, xr, d, bi, prev, lane);
     }
   }
-  if (lane == 0 && mine)
-    __hip_atomic_fetch_add(&blk_count, mine, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-  __syncthreads();
-  if (threadIdx.x == 0 && blk_count)
-    atomicAdd((unsigned long long *)&v.hdr->rechecked_total, blk_count);
-  if (amode == AM_LDS) flush_lds_acc(lds_acc, acc, k, d);
+  recheck_finish_count(mine, &blk_count, v);
+  if (amode & AM_INLDS) flush_lds_acc(lds_acc, acc, k, d);
 }
 
 __global__ void k_add(double *__restrict__ y, const double *__restrict__ x,
@@ -637,6 +852,11 @@ static unsigned grid_for(int64_t n, const void *kern, int block, size_t lds) {
 }
 
 // acc_kind: 0 = none (predict), 1 = full accumulation, 2 = delta
+static int acc_mode(int acc_kind, bool lds_fits) {
+  if (acc_kind == 0) return AM_NONE;
+  return AM_ON | (acc_kind == 2 ? AM_DELTA : 0) | (lds_fits ? AM_INLDS : 0);
+}
+
 template <class TX>
 static int launch_exact(const TX *X, int64_t n, int d, int64_t ldx,
                         const double *C, int k, int32_t *labels, double *acc,
@@ -646,14 +866,9 @@ static int launch_exact(const TX *X, int64_t n, int d, int64_t ldx,
   const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
   const int maxd = pick_maxd(d);
   const bool creg = maxd > 0 && c_bytes <= LDS_BUDGET;
-  int amode = AM_NONE;
-  if (acc_kind == 2) {
-    amode = AM_DELTA;
-  } else if (acc_kind == 1) {
-    const size_t base = creg ? c_bytes : 0;
-    amode = (base + a_bytes <= LDS_BUDGET) ? AM_LDS : AM_GLOBAL;
-  }
-  const size_t lds = (creg ? c_bytes : 0) + (amode == AM_LDS ? a_bytes : 0);
+  const size_t base = creg ? c_bytes : 0;
+  const int amode = acc_mode(acc_kind, base + a_bytes <= LDS_BUDGET);
+  const size_t lds = base + ((amode & AM_INLDS) ? a_bytes : 0);
   if (creg) {
 #define DKM_EXACT_CASE(M)                                                   \
   case M: {                                                                 \
@@ -735,30 +950,71 @@ static int launch_screen_nks(const TX *X, int64_t end, int d, int64_t ldx,
   return fail(DKM_E_ARG, "screen: d too large");
 }
 
+template <int MAXD, bool VEC, class TX>
+static void launch_recheck_lane_t(unsigned g, size_t lds, hipStream_t s,
+                                  const TX *X, int64_t end, int d,
+                                  int64_t ldx, int k, const WsView &v,
+                                  int32_t *lab_out, double *acc, int amode,
+                                  int64_t base) {
+  k_recheck_lane<MAXD, VEC, TX><<<g, BLOCK, lds, s>>>(X, end, d, ldx, k, v,
+                                                       lab_out, acc, amode,
+                                                       base);
+}
+
+template <int MAXD, class TX>
+static const void *recheck_lane_fn(bool vec) {
+  return vec ? (const void *)k_recheck_lane<MAXD, true, TX>
+             : (const void *)k_recheck_lane<MAXD, false, TX>;
+}
+
 template <class TX>
-static int launch_recheck_scan(const TX *X, int64_t end, int d, int64_t ldx,
-                               int k, const WsView &v, int32_t *lab_out,
-                               double *acc, int acc_kind, int64_t base,
-                               hipStream_t s) {
-  int amode = AM_NONE;
-  size_t lds = 0;
-  if (acc_kind == 2) {
-    amode = AM_DELTA;
-  } else if (acc_kind == 1) {
-    const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
-    amode = a_bytes <= LDS_BUDGET ? AM_LDS : AM_GLOBAL;
-    lds = amode == AM_LDS ? a_bytes : 0;
-  }
-  const int64_t waves = (end - base + 63) / 64;
+static int launch_recheck(const TX *X, int64_t end, int d, int64_t ldx, int k,
+                          const WsView &v, int32_t *lab_out, double *acc,
+                          int acc_kind, bool vec, int64_t base,
+                          hipStream_t s) {
+  const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
+  const size_t fb = recheck_lane_lds(k, d);
+  const bool lane = d <= 128 && fb <= LDS_BUDGET;
+  const int maxd = d <= 32 ? 32 : d <= 64 ? 64 : 128;
+  const size_t fixed = lane ? fb : 0;
+  const int amode = acc_mode(acc_kind, fixed + a_bytes <= LDS_BUDGET);
+  const size_t lds = fixed + ((amode & AM_INLDS) ? a_bytes : 0);
+  const bool small = d <= 128;
+  const void *kf =
+      !lane   ? (small ? (const void *)k_recheck_exact<true, TX>
+                       : (const void *)k_recheck_exact<false, TX>)
+      : maxd == 32 ? recheck_lane_fn<32, TX>(vec)
+      : maxd == 64 ? recheck_lane_fn<64, TX>(vec)
+                   : recheck_lane_fn<128, TX>(vec);
+  int per_cu = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, BLOCK, lds) !=
+          hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const int64_t waves = (end - base + 3 + (lane ? 255 : 63)) / (lane ? 256 : 64);
   const unsigned g = (unsigned)std::max<int64_t>(
-      1, std::min<int64_t>((int64_t)dev_info().cus * 4,
+      1, std::min<int64_t>((int64_t)dev_info().cus * per_cu,
                            (waves + BLOCK / 64 - 1) / (BLOCK / 64)));
-  if (d <= 128)
-    k_recheck_scan<true, TX><<<g, BLOCK, lds, s>>>(X, end, d, ldx, k, v,
-                                                   lab_out, acc, amode, base);
-  else
-    k_recheck_scan<false, TX><<<g, BLOCK, lds, s>>>(X, end, d, ldx, k, v,
-                                                    lab_out, acc, amode, base);
+  if (lane) {
+#define DKM_RL(M)                                                            \
+  (vec ? launch_recheck_lane_t<M, true, TX>(g, lds, s, X, end, d, ldx, k, v, \
+                                            lab_out, acc, amode, base)       \
+       : launch_recheck_lane_t<M, false, TX>(g, lds, s, X, end, d, ldx, k,   \
+                                             v, lab_out, acc, amode, base))
+    if (maxd == 32)
+      DKM_RL(32);
+    else if (maxd == 64)
+      DKM_RL(64);
+    else
+      DKM_RL(128);
+#undef DKM_RL
+  } else if (small) {
+    k_recheck_exact<true, TX><<<g, BLOCK, lds, s>>>(X, end, d, ldx, k, v,
+                                                     lab_out, acc, amode, base);
+  } else {
+    k_recheck_exact<false, TX><<<g, BLOCK, lds, s>>>(X, end, d, ldx, k, v,
+                                                      lab_out, acc, amode, base);
+  }
   return check_launch("exact re-check");
 }
 
@@ -777,12 +1033,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const int64_t chunk = labels ? n : nq;
   const size_t fb = screen_lds_fixed(k, d);
   const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
-  int amode = AM_NONE;
-  if (acc_kind == 2)
-    amode = AM_DELTA;
-  else if (acc_kind == 1)
-    amode = (fb + a_bytes <= LDS_BUDGET) ? AM_LDS : AM_GLOBAL;
-  const size_t lds = fb + (amode == AM_LDS ? a_bytes : 0);
+  const int amode = acc_mode(acc_kind, fb + a_bytes <= LDS_BUDGET);
+  const size_t lds = fb + ((amode & AM_INLDS) ? a_bytes : 0);
   const bool vec = (d % 8 == 0) && (ldx % (16 / (int64_t)sizeof(TX)) == 0) &&
                    (((uintptr_t)X % 16) == 0);
   for (int64_t base = 0; base < n; base += chunk) {
@@ -804,8 +1056,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                                                    lab_out, acc, amode, base,
                                                    lds, s);
     if (r) return r;
-    if ((r = launch_recheck_scan<TX>(X, end, d, ldx, k, v, lab_out, acc,
-                                     acc_kind, base, s)))
+    if ((r = launch_recheck<TX>(X, end, d, ldx, k, v, lab_out, acc,
+                                acc_kind, vec, base, s)))
       return r;
   }
   return 0;

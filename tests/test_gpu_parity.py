@@ -247,7 +247,9 @@ def _partial_sum_gpu(x, C, mode):
     (3000, 2, 3, 0), (4000, 7, 5, 1), (4000, 8, 9, 2), (5000, 13, 17, 3),
     (5000, 32, 100, 4), (3000, 50, 10, 5), (3000, 64, 40, 6),
     (2000, 100, 12, 7), (1000, 129, 8, 8), (600, 300, 5, 9),
-    (257, 1024, 33, 10), (4097, 1, 2, 11), (70, 3, 1, 12)])
+    (257, 1024, 33, 10), (4097, 1, 2, 11), (70, 3, 1, 12),
+    (3000, 32, 300, 13), (3000, 16, 250, 14), (2000, 100, 193, 15),
+    (2000, 32, 600, 16)])
 def test_partial_sum_vs_oracle(mode, n, d, k, seed):
     rng = np.random.default_rng(seed)
     x = rng.standard_normal((n, d)) * rng.uniform(0.5, 20)
@@ -369,7 +371,8 @@ def test_large_fit_properties():
 # incremental (delta) assignment used by the fit loop
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("mode", MODES)
-@pytest.mark.parametrize("d,k", [(32, 100), (7, 5), (64, 40)])
+@pytest.mark.parametrize("d,k", [(32, 100), (7, 5), (64, 40), (16, 300),
+                                 (130, 9)])
 def test_assign_delta_equals_difference_of_partial_sums(mode, d, k):
     from dislib_amd import _device, _lib
     rng = np.random.default_rng(d * 100 + k)
@@ -466,3 +469,45 @@ def test_screen_stress_vs_exact_kernel(mode):
         _device.predict(dd, C, ws, lab, m)
         bad = int((lab != ref).sum().item())
         assert bad == 0, "%d predict labels differ (rep %d)" % (bad, rep)
+
+
+@pytest.mark.parametrize("offset", [0, 1, 2, 3])
+@pytest.mark.parametrize("kind", ["partial", "delta", "predict"])
+def test_recheck_scan_misaligned_labels(offset, kind):
+    """Label arrays that are views at any int32 offset (not 16-B aligned),
+    with every sample sent to the re-check (exact ties) and n not a multiple
+    of 4: the re-check's int4 label scan must neither skip nor invent
+    samples at either end."""
+    from dislib_amd import _device, _lib
+    rng = np.random.default_rng(40 + offset)
+    d, n = 16, 9999
+    C = rng.standard_normal((6, d))
+    C[1] = C[0].copy()
+    C[1][0] = -C[0][0]
+    x = rng.standard_normal((n, d))
+    x[:, 0] = 0.0                 # exact ties between centres 0 and 1
+    x[::7] += 3.0                 # and some decided samples in between
+    dev = torch.device("cuda")
+    ds = _load(x, n)
+    dd = ds._device_data()
+    Ct = torch.from_numpy(C).to(dev)
+    ws = _device.Workspace(6, d, n, dev)
+    acc = torch.zeros(6 * (d + 1), dtype=torch.float64, device=dev)
+    big = torch.full((n + 8,), -1, dtype=torch.int32, device=dev)
+    lab = big[offset:offset + n]
+    _device.prepare(Ct, ws, acc)
+    if kind == "partial":
+        _device.partial_sum(dd, Ct, ws, lab, acc, _lib.MODE_BF16X3)
+    elif kind == "delta":
+        _device.assign_delta(dd, Ct, ws, lab, acc, _lib.MODE_BF16X3)
+    else:
+        _device.predict(dd, Ct, ws, lab, _lib.MODE_BF16X3)
+    rl, rs, rc = orc.partial_sum(x, C)
+    assert np.array_equal(lab.cpu().numpy(), rl)
+    b = big.cpu().numpy()
+    assert (b[:offset] == -1).all() and (b[offset + n:] == -1).all()
+    if kind != "predict":   # delta from "no previous label" == full sums
+        a = acc.cpu().numpy()
+        assert np.array_equal(a[6 * d:], rc.astype(np.float64))
+        _close(a[:6 * d].reshape(6, d), rs, 1e-12)
+    assert _device.rechecked(ws) > n // 2
