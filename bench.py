@@ -183,13 +183,16 @@ def main():
     bytes_per_launch = n * d * 8 + (n * 4 if a.labels else 0)
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     flops = 2.0 * k * d * n
+    # HBM bytes per launch from the committed PMC passes (tools/pmc_session.sh
+    # -> tools/pmc_summary.py --traffic-out), scaled to this launch's rows
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
-            if tj.get("n") == n and tj.get("d") == d and tj.get("k") == k:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
+            if tj.get("d") == d and tj.get("k") == k:
+                traffic = n * (tj["hbm_read_bytes_per_sample"] +
+                               tj["hbm_write_bytes_per_sample"])
+        except (OSError, ValueError, KeyError):
             traffic = None
     out = {
         "metric": METRIC,

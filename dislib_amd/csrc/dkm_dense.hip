@@ -42,6 +42,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "dkm_internal.h"
@@ -50,6 +52,7 @@ namespace dkm {
 
 constexpr int BLOCK = 256;
 constexpr size_t LDS_BUDGET = 80 * 1024;  // per block -> >= 2 blocks / CU
+constexpr size_t LDS_PER_CU = 160 * 1024;
 
 // Accumulation mode bits: AM_ON (accumulate at all), AM_DELTA (incremental:
 // only label changes move rows), AM_INLDS (block-private LDS accumulators,
@@ -74,6 +77,40 @@ static DevInfo dev_info() {
     cached_dev = dev;
   }
   return info;
+}
+
+// Workgroups of `block` threads resident per CU, for sizing the persistent
+// (grid-stride) grids: the smallest of the VGPR-file limit (512 registers
+// per lane per SIMD, 8-register granule, at most 6 waves per SIMD for the
+// ~100-SGPR kernels here), the LDS limit (160 KiB per CU) and 32 waves per
+// CU (MI355X_MICROARCH.md "Register files", "Residency").  The occupancy
+// API answered 1 for the 512-thread screen where 3 fit (2 instead of 6
+// waves per SIMD), so it is not used.  DKM_BLOCKS_PER_CU overrides, and
+// DKM_VERBOSE prints the numbers.
+static int resident_blocks(const void *kf, int block, size_t lds) {
+  if (const char *e = getenv("DKM_BLOCKS_PER_CU")) {
+    const int v = atoi(e);
+    if (v > 0) return v;
+  }
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, kf) != hipSuccess) return 1;
+  const int waves = (block + 63) / 64;
+  const int alloc = std::max(8, (fa.numRegs + 7) / 8 * 8);
+  const int wps = std::min(6, 512 / alloc);
+  const int by_regs = (4 * wps) / waves;
+  const size_t l = lds + fa.sharedSizeBytes;
+  const int by_lds = l ? (int)(LDS_PER_CU / l) : 32;
+  const int own =
+      std::max(1, std::min(std::min(by_regs, by_lds), 32 / waves));
+  if (getenv("DKM_VERBOSE")) {
+    int api = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&api, kf, block, lds) !=
+        hipSuccess)
+      api = -1;
+    fprintf(stderr, "dkm: block %d lds %zu vgpr %d -> %d/CU (api %d)\n",
+            block, l, fa.numRegs, own, api);
+  }
+  return own;
 }
 
 template <class TX>
@@ -268,41 +305,77 @@ __global__ void __launch_bounds__(BLOCK)
 // bound B on |(s_j + |x|^2) - numpy_dist_j^2|, and the exact re-check of
 // every sample whose best two scores are not 2B apart.
 //
+// The centre fragments hold -2c (exact scaling) and each MFMA chain starts
+// from |c|^2, so the chain's output IS the score (no VALU epilogue).
+//
 // Precisions (PREC):
 //   P_F32  v_mfma_f32_16x16x4_f32 (exact f32 fma chains) on x32 = fl32(x),
 //          c32 = fl32(c).  Bound: conversions 2u|x.c|, the d-term chain
-//          d*u*sum|x c|, fp32 |c|^2 (u|c|^2), final fma (u|s|), u = 2^-24.
-//   P_B3   v_mfma_f32_16x16x32_bf16 on bf16 hi/lo splits of x32 and c:
+//          d*u*(|c|^2 + sum|2 x c|), fp32 |c|^2 (u|c|^2), u = 2^-24.
+//   P_B3   v_mfma_f32_16x16x32_bf16 on bf16 hi/lo splits of x32 and -2c:
 //          x.c ~ xh.ch + xh.cl + xl.ch (products exact in fp32); split
 //          remainder <= 3.1 * 2^-16 sum|x c| (incl. the x -> x32 rounding),
-//          fp32 accumulation of 3d products bounded as (3d + 6) roundings of
-//          2^-23 (no assumption about the MFMA's internal adder), fp32
-//          |c|^2 and final fma.
+//          fp32 accumulation of |c|^2 and 3d products bounded as (3d + 6)
+//          roundings of 2^-23 (no assumption about the MFMA's internal
+//          adder), fp32 |c|^2.
 // Both doubled for safety, plus numpy's fp64 rounding (16 * 2^-52 (|x| +
 // cmax)^2), an absolute underflow floor, and |x.c| <= |x| cmax.  |x| is
 // computed in fp32 and inflated (relative error <= (d + 4) 2^-24).
+//
+// Index packing: the screen replaces the low PACK_BITS mantissa bits of each
+// score by the centre's index within its group of 128 centres, so one v_min
+// and one v_med3 per score keep a top-2 of (value, index) pairs.  Packing
+// moves a score by < 2^PACK_BITS ulp <= 2^-16 |s|, |s| <= |c|^2 + 2|x||c|;
+// `packed` adds that to B (both compared scores move, and the test is
+// s2 - s1 > 2B).
 // ---------------------------------------------------------------------------
 enum { P_F32 = 0, P_B3 = 1 };
 
+constexpr uint32_t PACK_BITS = 7;
+constexpr uint32_t PACK_MASK = (1u << PACK_BITS) - 1;
+constexpr int GROUP_BLOCKS = 1 << (PACK_BITS - 4);  // 16-centre blocks/group
+
 template <int PREC>
-__device__ __forceinline__ float screen_bound(int d, float xn, float cm) {
+__device__ __forceinline__ float screen_bound(int d, float xn, float cm,
+                                              bool packed) {
   float rel;
   if (PREC == P_F32)
     rel = (d + 6.0f) * 0x1.0p-24f;
   else
     rel = 3.1f * 0x1.0p-16f + (3.0f * d + 6.0f) * 0x1.0p-23f;
   const float s = xn + cm;
-  float b = 2.0f * rel * (2.0f * xn * cm + cm * cm);
+  const float mag = 2.0f * xn * cm + cm * cm;
+  float b = 2.0f * rel * mag;
+  if (packed) b += 0x1.0p-16f * mag;
   b += 16.0f * 0x1.0p-52f * s * s;
   b += (8.0f * d) * 0x1.0p-120f * (s + 1.0f);
   return b * 1.0001f;  // covers the fp32 evaluation of this bound
+}
+
+__device__ __forceinline__ float pack_score(float s, uint32_t idx) {
+  return __uint_as_float((__float_as_uint(s) & ~PACK_MASK) | idx);
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int SB = 256;  // screen block: 4 waves
+#ifndef DKM_SB
+#define DKM_SB 512
+#endif
+// NB1: 16-sample blocks per wave step at d <= 32.  WPE: waves per SIMD the
+// d <= 32 screen is compiled for (6 -> <= 80 VGPRs -> three 512-thread
+// blocks per CU; NB1 = 2 needs ~150 VGPRs, one block per CU); d <= 64: 4.
+#ifndef DKM_NB1
+#define DKM_NB1 1
+#endif
+#ifndef DKM_WPE
+#define DKM_WPE 6
+#endif
+#define DKM_SCREEN_WPE(NKS) \
+  __attribute__((amdgpu_waves_per_eu( \
+      DKM_WPE <= 0 ? 1 : (NKS) == 1 ? DKM_WPE : (NKS) == 2 ? 4 : 1)))
+constexpr int SB = DKM_SB;  // screen block: SB/64 waves share one LDS image
 
 // Eight consecutive features t0..t0+7 of one row, as fp64.  VEC: d % 8 == 0
 // and 16-B aligned rows, so the 8 features are in range iff t0 < d.
@@ -333,22 +406,118 @@ __device__ __forceinline__ void load8(const TX *xr, int t0, int d,
   }
 }
 
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// One undecided sample per lane (the screen's tail and k_recheck_lane).
+// Stage 1 re-screens in fp32 VALU (x in VGPRs, fp32 centres `cl` of row
+// stride dp and |c|^2 `cnl`, in LDS or global memory) -- the P_F32
+// arithmetic and bound, ~2^-24 instead of bf16x3's ~2^-16 -- and keeps the
+// label when the best two scores are 2B apart.  Otherwise stage 2 runs the
+// reference arithmetic on the candidates only (score <= best + 2B: the
+// reference winner is always among them, and every other centre is
+// strictly farther after sqrt).  Writes lab_out[i] and moves
+// the row between the accumulators as amode says (prev = previous label).
+template <int MAXD, bool VEC, class TX>
+__device__ __forceinline__ void resolve_lane(
+    const TX *__restrict__ X, int64_t ldx, int d, int k, int64_t i, int prev,
+    const float *cl, const float *cnl, int dp, float cm, const double *ct64,
+    int32_t *lab_out, int amode, const AccTarget &at) {
+  const TX *xr = X + i * ldx;
+  float xf[MAXD];
+  float xx = 0.f;
+#pragma unroll
+  for (int b = 0; b < MAXD / 8; ++b) {
+    double o[8];
+    if (8 * b < d) {
+      load8<VEC>(xr, 8 * b, d, o);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 8; ++m) o[m] = 0.0;
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      xf[8 * b + m] = (float)o[m];
+      xx = fmaf(xf[8 * b + m], xf[8 * b + m], xx);
+    }
+  }
+  // fp32 score of centre jc: fma chain over features (padding adds 0 * 0)
+  auto score = [&](int jc) {
+    const float *cr = cl + (int64_t)jc * dp;
+    float dot = 0.f;
+#pragma unroll
+    for (int t4 = 0; t4 < MAXD / 4; ++t4) {
+      if (4 * t4 < dp) {
+        const f32x4 c4 = *(const f32x4 *)(cr + 4 * t4);
+        dot = fmaf(xf[4 * t4 + 0], c4.x, dot);
+        dot = fmaf(xf[4 * t4 + 1], c4.y, dot);
+        dot = fmaf(xf[4 * t4 + 2], c4.z, dot);
+        dot = fmaf(xf[4 * t4 + 3], c4.w, dot);
+      }
+    }
+    return fmaf(-2.f, dot, cnl[jc]);
+  };
+  float b1 = INFINITY, b2 = INFINITY;
+  int i1 = 0;
+#pragma unroll 1
+  for (int jc = 0; jc < k; ++jc) {
+    const float sc = score(jc);
+    i1 = sc < b1 ? jc : i1;
+    b2 = __builtin_amdgcn_fmed3f(b1, b2, sc);
+    b1 = fminf(b1, sc);
+  }
+  const float xn = sqrtf(xx) * (1.0f + (d + 4) * 0x1.0p-24f);
+  const float B = screen_bound<P_F32>(d, xn, cm, false);
+  const bool sane = (xn < 1e18f) && (xn * cm < 1e30f) && (b1 < 1e30f);
+  int bi = i1;
+  if (!(sane && b2 - b1 > 2.0f * B)) {
+    const float lim = b1 + 2.0f * B;
+    double best = INFINITY;
+    bi = -1;
+#pragma unroll 1
+    for (int jc = 0; jc < k; ++jc) {
+      if (sane && !(score(jc) <= lim)) continue;
+      const SqDiffT<TX> f{xr, ct64 + jc, (int64_t)k};
+      const double dist = sqrt(pw_leaf(f, 0, d));
+      if (dist < best || bi < 0) {
+        best = dist;
+        bi = jc;
+      }
+    }
+  }
+  lab_out[i] = bi;
+  if (!(amode & AM_ON)) return;
+  const bool delta = amode & AM_DELTA;
+  if (delta && bi == prev) return;
+  const bool sub = delta && prev >= 0;
+  for (int t = 0; t < d; ++t) {
+    const double x = ld_x(xr + t);
+    at.add(bi, t, x);
+    if (sub) at.add(prev, t, -x);
+  }
+  at.count(bi, 1.0);
+  if (sub) at.count(prev, -1.0);
+}
+
 // One wave = NB blocks of 16 samples per step.  Lane l = (q = l >> 4,
 // j = l & 15) holds features ks*32 + 8q + m (m < 8) of sample j of every
 // block (4 x 16-B loads per lane per 32 features).  Outside the full-
 // accumulation modes the fp64 tile registers are reloaded with the NEXT
 // step's rows as soon as they are converted, so one tile is in flight during
 // the MFMA/scoring of the current one.  The MFMA output gives lane (q, j)
-// the dots of centres cb*16 + 4q + i (i < 4) with sample j; each lane keeps a
-// top-2 (fma, cmp, cndmask, med3, min per score), two xor-shuffles merge the
-// four lanes of a sample.  lab_out[si] = label, or -(prev + 2) when the
-// screen cannot decide (the re-check resolves it; prev = -1 outside
-// AM_DELTA).
+// the scores of centres cb*16 + 4q + i (i < 4) with sample j; each lane
+// keeps a packed top-2 per group of 128 centres (v_and_or, v_med3, v_min
+// per score), merges it into a running (value, index) top-2 per group, and
+// two xor-shuffles merge the four lanes of a sample.  lab_out[si] = label,
+// or -(prev + 2) when the screen cannot decide (the re-check resolves it;
+// prev = -1 outside AM_DELTA).
 template <int PREC, int NKS, int NB, bool VEC, class TX>
-__global__ void __launch_bounds__(SB)
+__global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
     k_screen(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
              WsView v, int32_t *__restrict__ lab_out, double *acc, int amode,
-             int64_t base) {
+             int64_t base, int use_list) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int nkb = (int)(kpad16(k) / 16);
   // fragment region: nkb*NKS blocks of 2 KB (f32: 8 floats per lane;
@@ -372,15 +541,27 @@ __global__ void __launch_bounds__(SB)
   __syncthreads();
 
   const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
-  const int64_t wv = (int64_t)blockIdx.x * (SB / 64) + (threadIdx.x >> 6);
+  const int wid = threadIdx.x >> 6;
+  const int64_t wv = (int64_t)blockIdx.x * (SB / 64) + wid;
   const int64_t step = (int64_t)gridDim.x * (SB / 64) * 16 * NB;
+  const int64_t seg = (int64_t)blockIdx.x * (SB / 64) + wid;
+  int2 *wl = v.tlist + seg * TL_CAP;  // this wave's undecided samples
+  const bool listing = use_list && seg < TL_SEGS;
+  int tl_cnt = 0;   // wave-uniform: listed samples
+  int tl_over = 0;  // wave-uniform: undecided samples left for the re-check
 
   double tile[NB][NKS][8];
+  // delta: the previous labels of the tile's samples travel with the tile
+  // (a label load issued at use time exposed a full HBM latency per step)
+  int pv[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) pv[b] = -1;
   auto load_tile = [&](int64_t s0) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       int64_t si = s0 + 16 * b + j;
       si = si < n ? si : n - 1;  // clamp: always a readable row
+      if (delta) pv[b] = lab_out[si];
       const TX *xr = X + si * ldx;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
@@ -415,23 +596,29 @@ __global__ void __launch_bounds__(SB)
       xx[b] += __shfl_xor(xx[b], 16, WAVE);
       xx[b] += __shfl_xor(xx[b], 32, WAVE);
     }
+    int prv[NB];  // this step's previous labels (pv is refilled below)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) prv[b] = pv[b];
     // ---- the next step's rows stream in while this one computes ----
     const int64_t s_next = s0 + step;
+#ifndef DKM_DBG_NOLOAD
     if (!full_acc && s_next < n) load_tile(s_next);
+#endif
 
-    float b1[NB], b2[NB];
-    int i1[NB];
+    // running (value, centre index) top-2 of this lane over all groups
+    float r1[NB], r2[NB];
+    int ri[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      b1[b] = INFINITY;
-      b2[b] = INFINITY;
-      i1[b] = 0;
+      r1[b] = INFINITY;
+      r2[b] = INFINITY;
+      ri[b] = 0;
     }
-    // MFMA chain of centre block cb into acc[]; consumed one chain later so
-    // that the next block's MFMAs overlap this block's VALU scoring.
+    // MFMA chain of centre block cb into accv[], started from |c|^2; consumed
+    // one chain later so that the next block's MFMAs overlap this block's
+    // VALU scoring.
     auto chain = [&](int cb, f32x4 (&accv)[NB]) {
-#pragma unroll
-      for (int b = 0; b < NB; ++b) accv[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 c4 = *(const f32x4 *)(cn + cb * 16 + 4 * q);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         const char *blk = frag + ((int64_t)cb * NKS + ks) * 2048;
@@ -444,14 +631,15 @@ __global__ void __launch_bounds__(SB)
 #pragma unroll
             for (int b = 0; b < NB; ++b)
               accv[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                  a[m], xf[b][ks][m], accv[b], 0, 0, 0);
+                  a[m], xf[b][ks][m], (ks == 0 && m == 0) ? c4 : accv[b], 0,
+                  0, 0);
         } else {
           const bf16x8 ah = *(const bf16x8 *)(blk + lane * 16);
           const bf16x8 al = *(const bf16x8 *)(blk + 1024 + lane * 16);
 #pragma unroll
           for (int b = 0; b < NB; ++b)
-            accv[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, xh[b][ks],
-                                                              accv[b], 0, 0, 0);
+            accv[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                ah, xh[b][ks], ks == 0 ? c4 : accv[b], 0, 0, 0);
 #pragma unroll
           for (int b = 0; b < NB; ++b)
             accv[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, xl[b][ks],
@@ -463,63 +651,97 @@ __global__ void __launch_bounds__(SB)
         }
       }
     };
-    auto score = [&](int cb, const f32x4 (&accv)[NB]) {
-      const float4 cn4 = *(const float4 *)(cn + cb * 16 + 4 * q);
-      const float cnv[4] = {cn4.x, cn4.y, cn4.z, cn4.w};
-      const int cbase = cb * 16 + 4 * q;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        // scalar fmaf on purpose: no v_pk_*_f32 anywhere (see the header
-        // note on packed-VALU operand hazards; built -fno-slp-vectorize)
-        float sc[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) sc[b] = fmaf(-2.f, accv[b][i], cnv[i]);
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-          // b1 <= b2: new second = med3(b1, b2, s); ties -> b2 == b1
-          i1[b] = sc[b] < b1[b] ? cbase + i : i1[b];
-          b2[b] = __builtin_amdgcn_fmed3f(b1[b], b2[b], sc[b]);
-          b1[b] = fminf(b1[b], sc[b]);
-        }
-      }
-    };
-    f32x4 acc_a[NB], acc_b[NB];
-    chain(0, acc_a);
-    int cb = 0;
-    for (; cb + 2 <= nkb; cb += 2) {  // ping-pong: no runtime-indexed arrays
-      chain(cb + 1, acc_b);
-      score(cb, acc_a);
-      if (cb + 2 < nkb) chain(cb + 2, acc_a);
-      score(cb + 1, acc_b);
+#ifdef DKM_DBG_NOCOMPUTE
+    for (int b = 0; b < NB; ++b) {
+      r1[b] = xx[b];
+      r2[b] = 1e20f;
     }
-    if (cb < nkb) score(cb, acc_a);  // odd block count: final chain in acc_a
-    // merge the top-2 of the four lanes of a sample (first index on ties)
+#else
+    for (int g0 = 0; g0 < nkb; g0 += GROUP_BLOCKS) {
+      const int g1 = min(nkb, g0 + GROUP_BLOCKS);
+      float b1[NB], b2[NB];  // packed, this group
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        b1[b] = INFINITY;
+        b2[b] = INFINITY;
+      }
+      auto score = [&](int cb, const f32x4 (&accv)[NB]) {
+        const uint32_t ib = (uint32_t)((cb - g0) * 16 + 4 * q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            // scalar ops on purpose: no v_pk_*_f32 anywhere (see the header
+            // note on packed-VALU operand hazards; built -fno-slp-vectorize)
+            const float sp = pack_score(accv[b][i], ib + i);
+            // b1 <= b2: new second = med3(b1, b2, s)
+            b2[b] = __builtin_amdgcn_fmed3f(b1[b], b2[b], sp);
+            b1[b] = fminf(b1[b], sp);
+          }
+        }
+      };
+      f32x4 acc_a[NB], acc_b[NB];
+      chain(g0, acc_a);
+      int cb = g0;
+      for (; cb + 2 <= g1; cb += 2) {  // ping-pong: no runtime-indexed arrays
+        chain(cb + 1, acc_b);
+        score(cb, acc_a);
+        if (cb + 2 < g1) chain(cb + 2, acc_a);
+        score(cb + 1, acc_b);
+      }
+      if (cb < g1) score(cb, acc_a);  // odd block count: last chain in acc_a
+      // fold the group's packed top-2 into the running (value, index) top-2
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int gi = g0 * 16 + (int)(__float_as_uint(b1[b]) & PACK_MASK);
+        const bool nw = b1[b] < r1[b];
+        r2[b] = nw ? fminf(r1[b], b2[b]) : fminf(r2[b], b1[b]);
+        ri[b] = nw ? gi : ri[b];
+        r1[b] = nw ? b1[b] : r1[b];
+      }
+    }
+#endif
+    // merge the top-2 of the four lanes of a sample
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
 #pragma unroll
       for (int off = 16; off <= 32; off <<= 1) {
-        const float ob1 = __shfl_xor(b1[b], off, WAVE);
-        const float ob2 = __shfl_xor(b2[b], off, WAVE);
-        const int oi1 = __shfl_xor(i1[b], off, WAVE);
-        const bool other = ob1 < b1[b] || (ob1 == b1[b] && oi1 < i1[b]);
-        b2[b] = other ? fminf(b1[b], ob2) : fminf(b2[b], ob1);
-        i1[b] = other ? oi1 : i1[b];
-        b1[b] = other ? ob1 : b1[b];
+        const float ob1 = __shfl_xor(r1[b], off, WAVE);
+        const float ob2 = __shfl_xor(r2[b], off, WAVE);
+        const int oi1 = __shfl_xor(ri[b], off, WAVE);
+        const bool other = ob1 < r1[b] || (ob1 == r1[b] && oi1 < ri[b]);
+        r2[b] = other ? fminf(r1[b], ob2) : fminf(r2[b], ob1);
+        ri[b] = other ? oi1 : ri[b];
+        r1[b] = other ? ob1 : r1[b];
       }
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int64_t si = s0 + 16 * b + j;
-      if (si >= n) continue;
       const float xn = sqrtf(xx[b]) * (1.0f + (d + 4) * 0x1.0p-24f);
-      const float B = screen_bound<PREC>(d, xn, cm);
-      const bool sane = (xn < 1e18f) && (xn * cm < 1e30f);
-      const bool unique = sane && (b2[b] - b1[b] > 2.0f * B);
-      const int lab = i1[b];
-      int prev = -1;
-      if (delta) prev = lab_out[si];  // 16 lanes x 4 B, coalesced
-      if (q == 0) lab_out[si] = unique ? lab : -(prev + 2);
-      if (!unique) continue;  // label + sums by the re-check
+      const float B = screen_bound<PREC>(d, xn, cm, true);
+      const bool sane = (xn < 1e18f) && (xn * cm < 1e30f) && (r1[b] < 1e30f);
+      const bool unique = sane && (r2[b] - r1[b] > 2.0f * B);
+      const bool und = si < n && !unique;
+      const int prev = delta ? prv[b] : -1;
+      // undecided samples join the wave's list (resolved in the tail) while
+      // it has room; the rest are counted for the re-check pass
+      const uint64_t um = __ballot(q == 0 && und);
+      const int add = __popcll(um);
+      if (listing && tl_cnt + add <= TL_CAP) {
+        if (q == 0 && und)
+          wl[tl_cnt + __popcll(um & ((1ull << lane) - 1))] =
+              make_int2((int)(si - base), prev);
+        tl_cnt += add;
+      } else {
+        tl_over += add;
+      }
+      if (si >= n) continue;
+      const int lab = ri[b];
+      // an unchanged delta label is already in place: no store
+      if (q == 0 && !(unique && lab == prev))
+        lab_out[si] = unique ? lab : -(prev + 2);
+      if (!unique) continue;  // label + sums by the tail / re-check
       if (full_acc) {
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks)
@@ -550,6 +772,10 @@ __global__ void __launch_bounds__(SB)
       }
     }
     if (full_acc && s_next < n) load_tile(s_next);  // the tile was in use
+  }
+  if (lane == 0) {
+    if (listing) v.tcount[seg] = tl_cnt;
+    if (tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
   }
   if (amode & AM_INLDS) {
     __syncthreads();
@@ -604,11 +830,6 @@ __device__ __forceinline__ void recheck_finish_count(
 
 constexpr int RL_CAP = 128;  // per-wave list: a full batch + one chunk
 
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
 static size_t recheck_lane_lds(int64_t k, int64_t d) {
   const int64_t dp = round_up(d, 4);
   return (size_t)round_up((k * dp + k) * 4, 8) +
@@ -620,6 +841,7 @@ __global__ void __launch_bounds__(BLOCK)
     k_recheck_lane(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
                    int k, WsView v, int32_t *__restrict__ lab_out,
                    double *acc, int amode, int64_t base) {
+  if (v.hdr->qcount == 0) return;  // the screen resolved everything
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int dp = (int)round_up(d, 4);  // c32 row stride (dkm_util)
   float *cl = (float *)smem;           // fp32 centres, k x dp (zero padded)
@@ -645,81 +867,9 @@ __global__ void __launch_bounds__(BLOCK)
   const int lane = threadIdx.x & 63;
   int64_t *wl = lists + (threadIdx.x >> 6) * RL_CAP;
 
-  // one undecided sample per lane
   auto resolve = [&](int64_t i) {
-    const int prev = -lab_out[i] - 2;
-    const TX *xr = X + i * ldx;
-    float xf[MAXD];
-    float xx = 0.f;
-#pragma unroll
-    for (int b = 0; b < MAXD / 8; ++b) {
-      double o[8];
-      if (8 * b < d) {
-        load8<VEC>(xr, 8 * b, d, o);
-      } else {
-#pragma unroll
-        for (int m = 0; m < 8; ++m) o[m] = 0.0;
-      }
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        xf[8 * b + m] = (float)o[m];
-        xx = fmaf(xf[8 * b + m], xf[8 * b + m], xx);
-      }
-    }
-    // fp32 score of centre j: fma chain over features (padding adds 0 * 0)
-    auto score = [&](int j) {
-      const float *cr = cl + (int64_t)j * dp;
-      float dot = 0.f;
-#pragma unroll
-      for (int t4 = 0; t4 < MAXD / 4; ++t4) {
-        if (4 * t4 < dp) {
-          const f32x4 c4 = *(const f32x4 *)(cr + 4 * t4);
-          dot = fmaf(xf[4 * t4 + 0], c4.x, dot);
-          dot = fmaf(xf[4 * t4 + 1], c4.y, dot);
-          dot = fmaf(xf[4 * t4 + 2], c4.z, dot);
-          dot = fmaf(xf[4 * t4 + 3], c4.w, dot);
-        }
-      }
-      return fmaf(-2.f, dot, cnl[j]);
-    };
-    float b1 = INFINITY, b2 = INFINITY;
-    int i1 = 0;
-    for (int j = 0; j < k; ++j) {
-      const float sc = score(j);
-      i1 = sc < b1 ? j : i1;
-      b2 = __builtin_amdgcn_fmed3f(b1, b2, sc);
-      b1 = fminf(b1, sc);
-    }
-    const float xn = sqrtf(xx) * (1.0f + (d + 4) * 0x1.0p-24f);
-    const float B = screen_bound<P_F32>(d, xn, cm);
-    const bool sane = (xn < 1e18f) && (xn * cm < 1e30f) && (b1 < 1e30f);
-    int bi = i1;
-    if (!(sane && b2 - b1 > 2.0f * B)) {
-      const float lim = b1 + 2.0f * B;
-      double best = INFINITY;
-      bi = -1;
-      for (int j = 0; j < k; ++j) {
-        if (sane && !(score(j) <= lim)) continue;
-        const SqDiffT<TX> f{xr, v.ct64 + j, (int64_t)k};
-        const double dist = sqrt(pw_leaf(f, 0, d));
-        if (dist < best || bi < 0) {
-          best = dist;
-          bi = j;
-        }
-      }
-    }
-    lab_out[i] = bi;
-    if (!(amode & AM_ON)) return;
-    const bool delta = amode & AM_DELTA;
-    if (delta && bi == prev) return;
-    const bool sub = delta && prev >= 0;
-    for (int t = 0; t < d; ++t) {
-      const double x = ld_x(xr + t);
-      at.add(bi, t, x);
-      if (sub) at.add(prev, t, -x);
-    }
-    at.count(bi, 1.0);
-    if (sub) at.count(prev, -1.0);
+    resolve_lane<MAXD, VEC, TX>(X, ldx, d, k, i, -lab_out[i] - 2, cl, cnl, dp,
+                                cm, v.ct64, lab_out, amode, at);
   };
 
   // Scan: 4 labels per lane (int4), 256 per wave step, the next step's
@@ -776,11 +926,60 @@ __global__ void __launch_bounds__(BLOCK)
   if (amode & AM_INLDS) flush_lds_acc(lds_acc, acc, k, d);
 }
 
+// The screen's per-wave lists (WsView::tlist/tcount, nseg segments): lane
+// per listed sample (resolve_lane), fp32 centres in LDS.  No label scan:
+// the work is proportional to the undecided samples only.
+template <int MAXD, bool VEC, class TX>
+__global__ void __launch_bounds__(BLOCK)
+    k_recheck_list(const TX *__restrict__ X, int d, int64_t ldx, int k,
+                   WsView v, int32_t *__restrict__ lab_out, double *acc,
+                   int amode, int64_t base, int nseg) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int dp = (int)round_up(d, 4);
+  float *cl = (float *)smem;           // fp32 centres, k x dp (zero padded)
+  float *cnl = cl + (int64_t)k * dp;   // |c|^2 fp32
+  double *lds_acc =
+      (double *)((char *)smem + round_up(((int64_t)k * dp + k) * 4, 8));
+  __shared__ unsigned long long blk_count;
+  if (threadIdx.x == 0) blk_count = 0;
+  {
+    const f32x4 *src = (const f32x4 *)v.c32;
+    f32x4 *dst = (f32x4 *)cl;
+    for (int64_t e = threadIdx.x; e < (int64_t)k * dp / 4; e += BLOCK)
+      dst[e] = src[e];
+    for (int e = threadIdx.x; e < k; e += BLOCK) cnl[e] = v.cn32[e];
+  }
+  if (amode & AM_INLDS) zero_lds_acc(lds_acc, k, d);
+  const float cm =
+      (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
+  const AccTarget at = acc_target(amode, lds_acc, acc, k, d);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+  const int64_t nwv = (int64_t)gridDim.x * (BLOCK / 64);
+  unsigned long long mine = 0;
+  for (int64_t sg = wv; sg < nseg; sg += nwv) {
+    const int cnt = v.tcount[sg];
+    mine += cnt;
+    const int2 *e = v.tlist + sg * TL_CAP;
+    for (int t0 = 0; t0 < cnt; t0 += 64) {
+      if (t0 + lane < cnt) {
+        const int2 it = e[t0 + lane];
+        resolve_lane<MAXD, VEC, TX>(X, ldx, d, k, base + it.x, it.y, cl, cnl,
+                                    dp, cm, v.ct64, lab_out, amode, at);
+      }
+    }
+  }
+  recheck_finish_count(mine, &blk_count, v);
+  if (amode & AM_INLDS) flush_lds_acc(lds_acc, acc, k, d);
+}
+
 template <bool SMALL, class TX>
 __global__ void __launch_bounds__(BLOCK)
     k_recheck_exact(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
                     int k, WsView v, int32_t *__restrict__ lab_out,
                     double *acc, int amode, int64_t base) {
+  if (v.hdr->qcount == 0) return;  // the screen resolved everything
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double *lds_acc = smem;
   __shared__ unsigned long long blk_count;
@@ -841,12 +1040,8 @@ static int pick_maxd(int d) {
 }
 
 static unsigned grid_for(int64_t n, const void *kern, int block, size_t lds) {
-  int per_cu = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block,
-                                                   lds) != hipSuccess ||
-      per_cu < 1)
-    per_cu = 1;
-  const int64_t cap = (int64_t)dev_info().cus * per_cu;
+  const int64_t cap =
+      (int64_t)dev_info().cus * resident_blocks(kern, block, lds);
   const int64_t need = (n + block - 1) / block;
   return (unsigned)std::max<int64_t>(1, std::min(need, cap));
 }
@@ -900,27 +1095,24 @@ static size_t screen_lds_fixed(int64_t k, int64_t d) {
 }
 
 static bool screen_ok(int64_t k, int64_t d) {
-  return k >= 2 && d <= 128 && screen_lds_fixed(k, d) <= LDS_BUDGET;
+  return k >= 2 && k <= 32767 && d <= 128 &&
+         screen_lds_fixed(k, d) <= LDS_BUDGET;
 }
 
 template <int PREC, int NKS, int NB, bool VEC, class TX>
 static int launch_screen_t(const TX *X, int64_t end, int d, int64_t ldx,
                            int k, const WsView &v, int32_t *lab_out,
                            double *acc, int amode, int64_t base, size_t lds,
-                           hipStream_t s) {
+                           int use_list, hipStream_t s, int *nseg) {
   const void *kf = (const void *)k_screen<PREC, NKS, NB, VEC, TX>;
-  int per_cu = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, SB, lds) !=
-          hipSuccess ||
-      per_cu < 1)
-    per_cu = 1;
-  const int64_t cap = (int64_t)dev_info().cus * per_cu;
+  const int64_t cap = (int64_t)dev_info().cus * resident_blocks(kf, SB, lds);
   const int64_t per_block = 16 * NB * (SB / 64);
   const int64_t need = (end - base + per_block - 1) / per_block;
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min(need, cap));
+  *nseg = (int)std::min<int64_t>((int64_t)g * (SB / 64), TL_SEGS);
   k_screen<PREC, NKS, NB, VEC, TX><<<g, SB, lds, s>>>(X, end, d, ldx, k, v,
                                                       lab_out, acc, amode,
-                                                      base);
+                                                      base, use_list);
   return check_launch("screen assignment");
 }
 
@@ -928,25 +1120,19 @@ template <int PREC, bool VEC, class TX>
 static int launch_screen_nks(const TX *X, int64_t end, int d, int64_t ldx,
                              int k, const WsView &v, int32_t *lab_out,
                              double *acc, int amode, int64_t base, size_t lds,
-                             hipStream_t s) {
+                             int use_list, hipStream_t s, int *nseg) {
+#define DKM_SCREEN_CASE(NKS, NB)                                             \
+  case NKS:                                                                  \
+    return launch_screen_t<PREC, NKS, NB, VEC, TX>(X, end, d, ldx, k, v,     \
+                                                   lab_out, acc, amode, base, \
+                                                   lds, use_list, s, nseg);
   switch (dpad32(d) / 32) {
-    case 1:
-      return launch_screen_t<PREC, 1, 2, VEC, TX>(X, end, d, ldx, k, v,
-                                                  lab_out, acc, amode, base,
-                                                  lds, s);
-    case 2:
-      return launch_screen_t<PREC, 2, 1, VEC, TX>(X, end, d, ldx, k, v,
-                                                  lab_out, acc, amode, base,
-                                                  lds, s);
-    case 3:
-      return launch_screen_t<PREC, 3, 1, VEC, TX>(X, end, d, ldx, k, v,
-                                                  lab_out, acc, amode, base,
-                                                  lds, s);
-    case 4:
-      return launch_screen_t<PREC, 4, 1, VEC, TX>(X, end, d, ldx, k, v,
-                                                  lab_out, acc, amode, base,
-                                                  lds, s);
+    DKM_SCREEN_CASE(1, DKM_NB1)
+    DKM_SCREEN_CASE(2, 1)
+    DKM_SCREEN_CASE(3, 1)
+    DKM_SCREEN_CASE(4, 1)
   }
+#undef DKM_SCREEN_CASE
   return fail(DKM_E_ARG, "screen: d too large");
 }
 
@@ -986,11 +1172,7 @@ static int launch_recheck(const TX *X, int64_t end, int d, int64_t ldx, int k,
       : maxd == 32 ? recheck_lane_fn<32, TX>(vec)
       : maxd == 64 ? recheck_lane_fn<64, TX>(vec)
                    : recheck_lane_fn<128, TX>(vec);
-  int per_cu = 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, BLOCK, lds) !=
-          hipSuccess ||
-      per_cu < 1)
-    per_cu = 1;
+  const int per_cu = resident_blocks(kf, BLOCK, lds);
   const int64_t waves = (end - base + 3 + (lane ? 255 : 63)) / (lane ? 256 : 64);
   const unsigned g = (unsigned)std::max<int64_t>(
       1, std::min<int64_t>((int64_t)dev_info().cus * per_cu,
@@ -1018,6 +1200,46 @@ static int launch_recheck(const TX *X, int64_t end, int d, int64_t ldx, int k,
   return check_launch("exact re-check");
 }
 
+template <int MAXD, bool VEC, class TX>
+static int launch_list_t(const TX *X, int d, int64_t ldx, int k,
+                         const WsView &v, int32_t *lab_out, double *acc,
+                         int amode, int64_t base, int nseg, size_t lds,
+                         hipStream_t s) {
+  const void *kf = (const void *)k_recheck_list<MAXD, VEC, TX>;
+  const int per_cu = resident_blocks(kf, BLOCK, lds);
+  const int64_t g = std::max<int64_t>(
+      1, std::min<int64_t>((int64_t)dev_info().cus * per_cu,
+                           (nseg + BLOCK / 64 - 1) / (BLOCK / 64)));
+  k_recheck_list<MAXD, VEC, TX><<<(unsigned)g, BLOCK, lds, s>>>(
+      X, d, ldx, k, v, lab_out, acc, amode, base, nseg);
+  return check_launch("list re-check");
+}
+
+// Can the listed samples be resolved lane-per-sample (k_recheck_list)?
+static bool list_ok(int64_t k, int64_t d) {
+  return d <= 128 && recheck_lane_lds(k, d) <= LDS_BUDGET;
+}
+
+template <class TX>
+static int launch_list(const TX *X, int d, int64_t ldx, int k,
+                       const WsView &v, int32_t *lab_out, double *acc,
+                       int acc_kind, bool vec, int64_t base, int nseg,
+                       hipStream_t s) {
+  const size_t fb = (size_t)round_up(((int64_t)k * round_up(d, 4) + k) * 4, 8);
+  const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
+  const int amode = acc_mode(acc_kind, fb + a_bytes <= LDS_BUDGET);
+  const size_t lds = fb + ((amode & AM_INLDS) ? a_bytes : 0);
+  const int maxd = d <= 32 ? 32 : d <= 64 ? 64 : 128;
+#define DKM_LL(M)                                                            \
+  (vec ? launch_list_t<M, true, TX>(X, d, ldx, k, v, lab_out, acc, amode,    \
+                                    base, nseg, lds, s)                      \
+       : launch_list_t<M, false, TX>(X, d, ldx, k, v, lab_out, acc, amode,   \
+                                     base, nseg, lds, s))
+  const int r = maxd == 32 ? DKM_LL(32) : maxd == 64 ? DKM_LL(64) : DKM_LL(128);
+#undef DKM_LL
+  return r;
+}
+
 // Screen + exact re-check over [0, n).  Labels go to `labels` when given,
 // else to the workspace scratch (queue region), in chunks of its capacity.
 template <class TX>
@@ -1037,25 +1259,29 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const size_t lds = fb + ((amode & AM_INLDS) ? a_bytes : 0);
   const bool vec = (d % 8 == 0) && (ldx % (16 / (int64_t)sizeof(TX)) == 0) &&
                    (((uintptr_t)X % 16) == 0);
+  const int use_list = list_ok(k, d) && !getenv("DKM_NO_LIST") ? 1 : 0;
   for (int64_t base = 0; base < n; base += chunk) {
     const int64_t end = std::min(n, base + chunk);
     int32_t *lab_out = labels ? labels : v.queue - base;
-    int r;
+    int r, nseg = 0;
     if (prec == P_F32)
       r = vec ? launch_screen_nks<P_F32, true, TX>(X, end, d, ldx, k, v,
                                                    lab_out, acc, amode, base,
-                                                   lds, s)
+                                                   lds, use_list, s, &nseg)
               : launch_screen_nks<P_F32, false, TX>(X, end, d, ldx, k, v,
                                                     lab_out, acc, amode, base,
-                                                    lds, s);
+                                                    lds, use_list, s, &nseg);
     else
       r = vec ? launch_screen_nks<P_B3, true, TX>(X, end, d, ldx, k, v,
                                                   lab_out, acc, amode, base,
-                                                  lds, s)
+                                                  lds, use_list, s, &nseg)
               : launch_screen_nks<P_B3, false, TX>(X, end, d, ldx, k, v,
                                                    lab_out, acc, amode, base,
-                                                   lds, s);
+                                                   lds, use_list, s, &nseg);
     if (r) return r;
+    if (use_list && (r = launch_list<TX>(X, d, ldx, k, v, lab_out, acc,
+                                         acc_kind, vec, base, nseg, s)))
+      return r;
     if ((r = launch_recheck<TX>(X, end, d, ldx, k, v, lab_out, acc,
                                 acc_kind, vec, base, s)))
       return r;

@@ -47,11 +47,19 @@ struct WsView {
   float *cn32;    // k fp32 ||c||^2 (computed in fp64, rounded once)
   double *cn64;   // k fp64 ||c||^2, sequential over t (sklearn row_norms)
   double *ct64;   // d x k transposed centres (DKM_PREP_CSR)
-  float *cfrag;   // fp32 centres in MFMA A-fragment order (see dkm_dense)
-  float *cnpad;   // kpad16 fp32 ||c||^2, +inf for padding centres
-  uint16_t *bfrag; // bf16 hi/lo centres in 16x16x32 MFMA fragment order
+  float *cfrag;   // fp32 -2*centres in MFMA A-fragment order (dkm_dense)
+  float *cnpad;   // kpad16 fp32 ||c||^2, 2^100 for padding centres
+  uint16_t *bfrag; // bf16 hi/lo of -2*centres, 16x16x32 fragment order
+  int2 *tlist;    // TL_SEGS x TL_CAP undecided (offset, prev) per screen wave
+  int32_t *tcount; // TL_SEGS entries used per screen wave
   int32_t *queue; // n_queue sample indices for the exact re-check
 };
+
+// Per-wave lists of the screen's undecided samples (resolved by
+// k_recheck_list without scanning the labels): one segment of TL_CAP
+// entries per screen wave, TL_SEGS >= 256 CUs x 32 waves.
+constexpr int TL_CAP = 256;
+constexpr int TL_SEGS = 8192;
 
 // MFMA fragment tiling of the centres: 16 centres x 16 dims per 1 KB block.
 __host__ __device__ inline int64_t kpad16(int64_t k) { return (k + 15) / 16 * 16; }

@@ -44,6 +44,8 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
   b += round_up(kpad16(k) * dpad32(d) * 4, 256);  // cfrag
   b += round_up(kpad16(k) * 4, 256);  // cnpad
   b += round_up(kpad16(k) * dpad32(d) * 4, 256);  // bfrag (hi + lo bf16)
+  b += (size_t)TL_SEGS * TL_CAP * 8;  // tlist
+  b += (size_t)TL_SEGS * 4;           // tcount
   b += round_up(n_queue * 4, 256);    // queue
   return b;
 }
@@ -68,6 +70,10 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   p += round_up(kpad16(k) * 4, 256);
   v->bfrag = (uint16_t *)p;
   p += round_up(kpad16(k) * dpad32(d) * 4, 256);
+  v->tlist = (int2 *)p;
+  p += (size_t)TL_SEGS * TL_CAP * 8;
+  v->tcount = (int32_t *)p;
+  p += (size_t)TL_SEGS * 4;
   v->queue = (int32_t *)p;
   const size_t fixed = (size_t)(p - (char *)ws);
   if (bytes < fixed + 256)
@@ -117,13 +123,16 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ C,
   }
 }
 
-// Centres in MFMA A-fragment order (dkm_dense k_screen).  Block (cb, ks) =
-// 16 centres x 32 features = 2 KB.  Lane l of a wave stands for centre
-// cb*16 + (l & 15) and features ks*32 + 8*(l >> 4) + m, m = 0..7:
+// Centres in MFMA A-fragment order (dkm_dense k_screen), pre-scaled by -2
+// (exact) so that the MFMA chain started from |c|^2 yields the score
+// |c|^2 - 2 x.c directly.  Block (cb, ks) = 16 centres x 32 features = 2 KB.
+// Lane l of a wave stands for centre cb*16 + (l & 15) and features
+// ks*32 + 8*(l >> 4) + m, m = 0..7:
 //  cfrag: 8 fp32 at l*32 B (v_mfma_f32_16x16x4_f32, k-step m);
 //  bfrag: 8 bf16 hi at l*16 B, 8 bf16 lo at 1024 + l*16 B
 //         (v_mfma_f32_16x16x32_bf16).
-// Zero padded; cnpad = +inf for padding centres.
+// Zero padded; cnpad = 2^100 for padding centres (finite: the screen packs
+// centre indices into the low mantissa bits of the scores).
 __global__ void __launch_bounds__(256) k_frag(const double *__restrict__ C,
                                               int64_t k, int64_t d, WsView v) {
   const int64_t nkb = kpad16(k) / 16, nks = dpad32(d) / 32;
@@ -135,9 +144,10 @@ __global__ void __launch_bounds__(256) k_frag(const double *__restrict__ C,
     const int l = (int)(w >> 3), m = (int)(w & 7);
     const int64_t c = cb * 16 + (l & 15);
     const int64_t t = ks * 32 + 8 * (l >> 4) + m;
-    const double x = (c < k && t < d) ? C[c * d + t] : 0.0;
+    const double x = (c < k && t < d) ? -2.0 * C[c * d + t] : 0.0;
     v.cfrag[blk * 512 + l * 8 + m] = (float)x;
-    // bf16x3 split: c = hi + lo + O(2^-16 |c|), hi = bf16(c), lo = bf16(c-hi)
+    // bf16x3 split of x = -2c: x = hi + lo + O(2^-16 |x|), hi = bf16(x),
+    // lo = bf16(x - hi)
     const __bf16 hi = (__bf16)(float)x;
     const __bf16 lo = (__bf16)(float)(x - (double)(float)hi);
     uint16_t *dst = v.bfrag + blk * 1024;
@@ -147,7 +157,7 @@ __global__ void __launch_bounds__(256) k_frag(const double *__restrict__ C,
   const int64_t kp = kpad16(k);
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < kp;
        c += (int64_t)gridDim.x * blockDim.x)
-    v.cnpad[c] = c < k ? v.cn32[c] : INFINITY;
+    v.cnpad[c] = c < k ? v.cn32[c] : 0x1.0p100f;
 }
 
 // ---------------------------------------------------------------------------

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build A/B variants of libdkm.so (screen-kernel compile-time knobs) next to
+# the default library: ../libdkm_<name>.so.  usage: bash variants.sh name "DEFS" ...
+set -e
+cd "$(dirname "$0")"
+while [ $# -ge 2 ]; do
+  name=$1; defs=$2; shift 2
+  d=build_$name; mkdir -p $d
+  for f in dkm_util dkm_dense dkm_sparse; do
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off \
+      -fno-slp-vectorize $defs -c $f.hip -o $d/$f.o &
+  done
+  wait
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../libdkm_$name.so $d/*.o
+  echo built ../libdkm_$name.so
+done

@@ -484,9 +484,11 @@ def test_recheck_scan_misaligned_labels(offset, kind):
     C = rng.standard_normal((6, d))
     C[1] = C[0].copy()
     C[1][0] = -C[0][0]
+    C[2:] += 10.0                 # far away: centres 0 and 1 are nearest
     x = rng.standard_normal((n, d))
     x[:, 0] = 0.0                 # exact ties between centres 0 and 1
-    x[::7] += 3.0                 # and some decided samples in between
+    # and some samples decided for centre 2 in between
+    x[::7] = C[2] + 0.1 * rng.standard_normal((len(x[::7]), d))
     dev = torch.device("cuda")
     ds = _load(x, n)
     dd = ds._device_data()

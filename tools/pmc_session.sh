@@ -5,10 +5,11 @@
 #   TARGET = <mode list>  -> tools/bench_modes.py --modes <list> on 20M rows
 TAG=${1:-r01}; TARGET=${2:-bench}; shift 2
 OUT=gpurun_out/${TAG}_pmc; mkdir -p $OUT; export TMPDIR=/tmp
+N=${PMC_N:-20000000}
 if [ "$TARGET" = bench ]; then
-  PROG=(python bench.py --n 20000000 --steps 8 --warmup 4 --no-cpu)
+  PROG=(python bench.py --n $N --steps 8 --warmup 4 --no-cpu)
 else
-  PROG=(python tools/bench_modes.py --n 20000000 --rounds 2 --modes $TARGET)
+  PROG=(python tools/bench_modes.py --n $N --rounds 2 --modes $TARGET)
 fi
 run() {  # name counters...
   local name=$1; shift
@@ -24,4 +25,6 @@ run p3 FETCH_SIZE
 run p3b WRITE_SIZE
 run p4 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_VALU_MFMA_BUSY_CYCLES
 run p5 TA_BUSY_avr TA_TA_BUSY_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum
+python tools/pmc_summary.py $OUT --n $N --traffic-out $OUT/traffic.json \
+  > $OUT/summary.txt 2>&1
 echo "== done"

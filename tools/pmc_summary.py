@@ -1,0 +1,83 @@
+"""Summarise rocprofv3 --pmc passes (tools/pmc_session.sh output) per kernel:
+mean counter value per dispatch, for the steady-state launches.
+
+  python tools/pmc_summary.py gpurun_out/<tag>_pmc [--skip N] [--json out]
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports 1/2 of the bytes of a
+wide (16 B/lane) streaming read, so reads are counted as 2 x FETCH_SIZE.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import re
+
+
+def short(name):
+    m = re.match(r"(?:void )?(?:dkm::)?([A-Za-z_0-9]+)", name)
+    return m.group(1) if m else name[:30]
+
+
+def load(d):
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(d, "*", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            per[k][r["Counter_Name"]].append(
+                (int(r["Dispatch_Id"]), float(r["Counter_Value"]),
+                 int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--skip", type=int, default=4,
+                    help="skip the first N launches of each kernel (warmup)")
+    ap.add_argument("--json")
+    ap.add_argument("--traffic-out",
+                    help="write per-sample HBM bytes of the assignment "
+                         "kernels (k_screen + k_recheck*) for bench.py")
+    ap.add_argument("--n", type=int, help="rows per launch of the profiled run")
+    ap.add_argument("--d", type=int, default=32)
+    ap.add_argument("--k", type=int, default=100)
+    a = ap.parse_args()
+    per = load(a.dir)
+    out = {}
+    for k, ctrs in sorted(per.items()):
+        row = {}
+        for c, vals in sorted(ctrs.items()):
+            vals = sorted(vals)
+            v = vals[a.skip:] if len(vals) > a.skip else vals
+            row[c] = sum(x[1] for x in v) / len(v)
+            row["_launches"] = len(v)
+        if "FETCH_SIZE" in row:
+            row["hbm_read_bytes"] = 2 * row["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in row:
+            row["hbm_write_bytes"] = row["WRITE_SIZE"] * 1024
+        out[k] = row
+        print(k)
+        for c, v in row.items():
+            print("   %-28s %.6g" % (c, v))
+    if a.json:
+        json.dump(out, open(a.json, "w"), indent=1)
+    if a.traffic_out:
+        ks = [k for k in out if k.startswith(("k_screen", "k_recheck"))]
+        rd = sum(out[k].get("hbm_read_bytes", 0.0) for k in ks)
+        wr = sum(out[k].get("hbm_write_bytes", 0.0) for k in ks)
+        json.dump({"kernels": ks, "n": a.n, "d": a.d, "k": a.k,
+                   "hbm_read_bytes_per_sample": rd / a.n,
+                   "hbm_write_bytes_per_sample": wr / a.n,
+                   "source": os.path.abspath(a.dir).split("/repo/")[-1],
+                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, "
+                             "KiB; reads x2 (gfx950 FETCH_SIZE = 1/2 of a "
+                             "wide streaming read, MI355X_MICROARCH.md "
+                             "HBM); mean over steady-state launches"},
+                  open(a.traffic_out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
