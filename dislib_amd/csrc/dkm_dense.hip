@@ -323,8 +323,11 @@ __global__ void __launch_bounds__(BLOCK)
 // computed in fp32 and inflated (relative error <= (d + 4) 2^-24).
 //
 // Index packing: the screen replaces the low PACK_BITS mantissa bits of each
-// score by the centre's index within its group of 128 centres, so one v_min
-// and one v_med3 per score keep a top-2 of (value, index) pairs.  Packing
+// score by a wave-uniform tag (16-centre block within its group of 32 blocks,
+// accumulator row i < 4); the lane's q supplies the rest of the centre index
+// (cb * 16 + 4q + i) when the group is folded.  One v_and_or, one v_med3 and
+// one v_min (med3 against -inf, no NaN canonicalisation) per score keep a
+// top-2 of (value, index) pairs.  Packing
 // moves a score by < 2^PACK_BITS ulp <= 2^-16 |s|, |s| <= |c|^2 + 2|x||c|;
 // `packed` adds that to B (both compared scores move, and the test is
 // s2 - s1 > 2B).
@@ -333,7 +336,7 @@ enum { P_F32 = 0, P_B3 = 1 };
 
 constexpr uint32_t PACK_BITS = 7;
 constexpr uint32_t PACK_MASK = (1u << PACK_BITS) - 1;
-constexpr int GROUP_BLOCKS = 1 << (PACK_BITS - 4);  // 16-centre blocks/group
+constexpr int GROUP_BLOCKS = 1 << (PACK_BITS - 2);  // 16-centre blocks/group
 
 template <int PREC>
 __device__ __forceinline__ float screen_bound(int d, float xn, float cm,
@@ -356,9 +359,92 @@ __device__ __forceinline__ float pack_score(float s, uint32_t idx) {
   return __uint_as_float((__float_as_uint(s) & ~PACK_MASK) | idx);
 }
 
+// A value the compiler cannot see through (a v_mov it must keep).  The
+// screen keeps -inf and the packing mask in VGPRs this way, so that
+// med3(a, b, -inf) stays one v_med3 (a visible -inf is folded into fminf,
+// which costs two NaN-canonicalising v_max) and the packing stays one
+// v_and_or_b32 with the wave-uniform tag in an SGPR.
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t v) {
+  uint32_t r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+__device__ __forceinline__ uint32_t opaque_s32(uint32_t v) {
+  uint32_t r;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "s"(v));
+  return r;
+}
+// min without fminf's NaN canonicalisation: the screen's NaN/Inf samples
+// are caught by its `sane` test either way.  ninf = opaque -inf.
+__device__ __forceinline__ float min_nc(float a, float b, float ninf) {
+  return __builtin_amdgcn_fmed3f(a, b, ninf);
+}
+
+// The two values x and x' of lane l and lane l ^ (16 or 32), in some order:
+// v_permlane{16,32}_swap instead of an LDS ds_bpermute round trip.  Callers
+// combine the pair symmetrically, so the order does not matter.
+template <int OFF>
+__device__ __forceinline__ void pair_xor(float x, float &a, float &b) {
+  const uint32_t u = __float_as_uint(x);
+  if constexpr (OFF == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+  }
+}
+template <int OFF>
+__device__ __forceinline__ void pair_xor(int x, int &a, int &b) {
+  float fa, fb;
+  pair_xor<OFF>(__int_as_float(x), fa, fb);
+  a = __float_as_int(fa);
+  b = __float_as_int(fb);
+}
+
+// Per-launch constants of screen_bound: 2B = k_mag * mag + k_s2 * s^2 +
+// k_s1 * (s + 1), s = xn + cm, mag = 2 xn cm + cm^2 (same terms, pre-summed;
+// the 1.0001 factor covers the fp32 evaluation of either form).
+struct BoundK {
+  float k_mag, k_s2, k_s1, two_cm, cm2, cm, xn_scale;
+};
+template <int PREC>
+__device__ __forceinline__ BoundK bound_consts(int d, float cm) {
+  float rel;
+  if (PREC == P_F32)
+    rel = (d + 6.0f) * 0x1.0p-24f;
+  else
+    rel = 3.1f * 0x1.0p-16f + (3.0f * d + 6.0f) * 0x1.0p-23f;
+  BoundK k;
+  k.k_mag = 2.0f * (2.0f * rel + 0x1.0p-16f) * 1.0001f;
+  k.k_s2 = 2.0f * 16.0f * 0x1.0p-52f * 1.0001f;
+  k.k_s1 = 2.0f * (8.0f * d) * 0x1.0p-120f * 1.0001f;
+  k.two_cm = 2.0f * cm;
+  k.cm2 = cm * cm;
+  k.cm = cm;
+  // v_sqrt_f32 (<= 1 ulp) instead of the correctly rounded sqrtf: 4 more ulp
+  k.xn_scale = 1.0f + (d + 8) * 0x1.0p-24f;
+  return k;
+}
+// 2B for a sample with fp32 |x|^2 = xx (packed scores)
+__device__ __forceinline__ float bound2_fast(const BoundK &k, float xx,
+                                            float &xn) {
+  xn = __builtin_amdgcn_sqrtf(__builtin_amdgcn_fmed3f(xx, 0x1.0p-100f,
+                                                      INFINITY)) *
+       k.xn_scale;
+  const float s = xn + k.cm;
+  const float mag = fmaf(xn, k.two_cm, k.cm2);
+  float b = k.k_mag * mag;
+  b = fmaf(k.k_s2 * s, s, b);
+  return fmaf(k.k_s1, s + 1.0f, b);
+}
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 #ifndef DKM_SB
 #define DKM_SB 512
@@ -535,13 +621,16 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
   }
   const float cm =
       (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
+  const BoundK bk = bound_consts<PREC>(d, cm);
+  const float ninf = __uint_as_float(opaque_u32(0xff800000u));
+  const uint32_t vmask = opaque_u32(~PACK_MASK);
   const bool full_acc = am_full(amode);
   const bool delta = amode & AM_DELTA;
   const AccTarget at = acc_target(amode, lds_acc, acc, k, d);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
-  const int wid = threadIdx.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t wv = (int64_t)blockIdx.x * (SB / 64) + wid;
   const int64_t step = (int64_t)gridDim.x * (SB / 64) * 16 * NB;
   const int64_t seg = (int64_t)blockIdx.x * (SB / 64) + wid;
@@ -556,7 +645,65 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
   int pv[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) pv[b] = -1;
+  // VEC steps: buffer loads off a per-step SGPR descriptor (base = the
+  // step's first row, 32-bit lane offsets, no 64-bit lane pointers); rows
+  // past n fall outside num_records and read as 0 (no clamp needed)
+  const bool off32 =
+      (int64_t)16 * NB * ldx * (int64_t)sizeof(TX) < (1ll << 31);
+  const uint32_t lane_off = (uint32_t)(j * ldx * (int64_t)sizeof(TX)) +
+                            (uint32_t)(8 * q * sizeof(TX));
   auto load_tile = [&](int64_t s0) {
+    if (VEC && off32) {
+      const int64_t rows = n - s0;
+      const int64_t xb = rows * ldx * (int64_t)sizeof(TX);
+      const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(X + s0 * ldx), 0,
+          (int)std::min<int64_t>(xb, 0x7fffffff), 0x00020000);
+      if (delta) {
+        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(lab_out + s0), 0,
+            (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          pv[b] = (int)__builtin_amdgcn_raw_buffer_load_b32(
+              rl, (16 * b + j) * 4, 0, 0);
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const uint32_t ob = lane_off + (uint32_t)(16 * b * ldx * sizeof(TX));
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          if (ks * 32 + 8 * q < d) {
+            const uint32_t o = ob + ks * 32 * sizeof(TX);
+            if constexpr (sizeof(TX) == 8) {
+#pragma unroll
+              for (int p4 = 0; p4 < 4; ++p4) {
+                const double2 v2 = __builtin_bit_cast(
+                    double2,
+                    __builtin_amdgcn_raw_buffer_load_b128(rx, o + 16 * p4, 0, 0));
+                tile[b][ks][2 * p4] = v2.x;
+                tile[b][ks][2 * p4 + 1] = v2.y;
+              }
+            } else {
+#pragma unroll
+              for (int p4 = 0; p4 < 2; ++p4) {
+                const float4 v4 = __builtin_bit_cast(
+                    float4,
+                    __builtin_amdgcn_raw_buffer_load_b128(rx, o + 16 * p4, 0, 0));
+                tile[b][ks][4 * p4] = v4.x;
+                tile[b][ks][4 * p4 + 1] = v4.y;
+                tile[b][ks][4 * p4 + 2] = v4.z;
+                tile[b][ks][4 * p4 + 3] = v4.w;
+              }
+            }
+          } else {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) tile[b][ks][m] = 0.0;
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       int64_t si = s0 + 16 * b + j;
@@ -582,19 +729,34 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          const float x32 = (float)tile[b][ks][m];
-          xx[b] = fmaf(x32, x32, xx[b]);
+        for (int m = 0; m < 8; m += 2) {
+          const float x0 = (float)tile[b][ks][m];
+          const float x1 = (float)tile[b][ks][m + 1];
+          xx[b] = fmaf(x0, x0, xx[b]);
+          xx[b] = fmaf(x1, x1, xx[b]);
           if constexpr (PREC == P_F32) {
-            xf[b][ks][m] = x32;
+            xf[b][ks][m] = x0;
+            xf[b][ks][m + 1] = x1;
           } else {
-            const __bf16 h = (__bf16)x32;
-            xh[b][ks][m] = h;
-            xl[b][ks][m] = (__bf16)(x32 - (float)h);  // exact subtraction
+            // one v_cvt_pk_bf16_f32 per pair; the hi parts back as fp32 by
+            // shift / mask; lo = x - hi is exact
+            const bf16x2 h2 = __builtin_convertvector(f32x2{x0, x1}, bf16x2);
+            const uint32_t hu = __builtin_bit_cast(uint32_t, h2);
+            const float h0 = __uint_as_float(hu << 16);
+            const float h1 = __uint_as_float(hu & 0xffff0000u);
+            const bf16x2 l2 =
+                __builtin_convertvector(f32x2{x0 - h0, x1 - h1}, bf16x2);
+            xh[b][ks][m] = h2[0];
+            xh[b][ks][m + 1] = h2[1];
+            xl[b][ks][m] = l2[0];
+            xl[b][ks][m + 1] = l2[1];
           }
         }
-      xx[b] += __shfl_xor(xx[b], 16, WAVE);
-      xx[b] += __shfl_xor(xx[b], 32, WAVE);
+      float xa, xb;
+      pair_xor<16>(xx[b], xa, xb);
+      xx[b] = xa + xb;
+      pair_xor<32>(xx[b], xa, xb);
+      xx[b] = xa + xb;
     }
     int prv[NB];  // this step's previous labels (pv is refilled below)
 #pragma unroll
@@ -666,17 +828,21 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
         b2[b] = INFINITY;
       }
       auto score = [&](int cb, const f32x4 (&accv)[NB]) {
-        const uint32_t ib = (uint32_t)((cb - g0) * 16 + 4 * q);
+        const uint32_t ib = (uint32_t)((cb - g0) * 4);  // wave-uniform tag
+        uint32_t tag[4];  // opaque SGPRs: one v_and_or_b32 per score
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tag[i] = opaque_s32(ib + i);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
 #pragma unroll
           for (int b = 0; b < NB; ++b) {
             // scalar ops on purpose: no v_pk_*_f32 anywhere (see the header
             // note on packed-VALU operand hazards; built -fno-slp-vectorize)
-            const float sp = pack_score(accv[b][i], ib + i);
+            const float sp = __uint_as_float(
+                (__float_as_uint(accv[b][i]) & vmask) | tag[i]);
             // b1 <= b2: new second = med3(b1, b2, s)
             b2[b] = __builtin_amdgcn_fmed3f(b1[b], b2[b], sp);
-            b1[b] = fminf(b1[b], sp);
+            b1[b] = min_nc(b1[b], sp, ninf);
           }
         }
       };
@@ -693,35 +859,45 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
       // fold the group's packed top-2 into the running (value, index) top-2
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
-        const int gi = g0 * 16 + (int)(__float_as_uint(b1[b]) & PACK_MASK);
+        const uint32_t tg = __float_as_uint(b1[b]) & PACK_MASK;
+        const int gi = (g0 + (int)(tg >> 2)) * 16 + 4 * q + (int)(tg & 3);
         const bool nw = b1[b] < r1[b];
-        r2[b] = nw ? fminf(r1[b], b2[b]) : fminf(r2[b], b1[b]);
+        r2[b] = nw ? min_nc(r1[b], b2[b], ninf) : min_nc(r2[b], b1[b], ninf);
         ri[b] = nw ? gi : ri[b];
         r1[b] = nw ? b1[b] : r1[b];
       }
     }
 #endif
     // merge the top-2 of the four lanes of a sample
+    // (symmetric in the pair: both lanes get the same result whichever
+    // order pair_xor hands the two sides over)
+    auto merge2 = [&](float &v1, float &v2, int &vi, float a1, float a2,
+                      int ai, float c1, float c2, int ci) {
+      const bool tc = (c1 < a1) | ((c1 == a1) & (ci < ai));
+      v1 = tc ? c1 : a1;
+      vi = tc ? ci : ai;
+      v2 = tc ? min_nc(a1, c2, ninf) : min_nc(a2, c1, ninf);
+    };
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-#pragma unroll
-      for (int off = 16; off <= 32; off <<= 1) {
-        const float ob1 = __shfl_xor(r1[b], off, WAVE);
-        const float ob2 = __shfl_xor(r2[b], off, WAVE);
-        const int oi1 = __shfl_xor(ri[b], off, WAVE);
-        const bool other = ob1 < r1[b] || (ob1 == r1[b] && oi1 < ri[b]);
-        r2[b] = other ? fminf(r1[b], ob2) : fminf(r2[b], ob1);
-        ri[b] = other ? oi1 : ri[b];
-        r1[b] = other ? ob1 : r1[b];
-      }
+      float a1, c1, a2, c2;
+      int ai, ci;
+      pair_xor<16>(r1[b], a1, c1);
+      pair_xor<16>(r2[b], a2, c2);
+      pair_xor<16>(ri[b], ai, ci);
+      merge2(r1[b], r2[b], ri[b], a1, a2, ai, c1, c2, ci);
+      pair_xor<32>(r1[b], a1, c1);
+      pair_xor<32>(r2[b], a2, c2);
+      pair_xor<32>(ri[b], ai, ci);
+      merge2(r1[b], r2[b], ri[b], a1, a2, ai, c1, c2, ci);
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int64_t si = s0 + 16 * b + j;
-      const float xn = sqrtf(xx[b]) * (1.0f + (d + 4) * 0x1.0p-24f);
-      const float B = screen_bound<PREC>(d, xn, cm, true);
-      const bool sane = (xn < 1e18f) && (xn * cm < 1e30f) && (r1[b] < 1e30f);
-      const bool unique = sane && (r2[b] - r1[b] > 2.0f * B);
+      float xn;
+      const float B2 = bound2_fast(bk, xx[b], xn);
+      const bool sane = (xn < 1e18f) & (xn * cm < 1e30f) & (r1[b] < 1e30f);
+      const bool unique = sane & (r2[b] - r1[b] > B2);
       const bool und = si < n && !unique;
       const int prev = delta ? prv[b] : -1;
       // undecided samples join the wave's list (resolved in the tail) while
