@@ -506,8 +506,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 // reference winner is always among them, and every other centre is
 // strictly farther after sqrt).  Writes lab_out[i] and moves
 // the row between the accumulators as amode says (prev = previous label).
-template <int MAXD, bool VEC, class TX>
-__device__ __forceinline__ void resolve_lane(
+// STAGE1_ONLY: return false (writing nothing) when stage 1 cannot decide,
+// so the caller can batch the rare stage-2 samples into full waves.
+template <int MAXD, bool VEC, class TX, bool STAGE1_ONLY = false>
+__device__ __forceinline__ bool resolve_lane(
     const TX *__restrict__ X, int64_t ldx, int d, int k, int64_t i, int prev,
     const float *cl, const float *cnl, int dp, float cm, const double *ct64,
     int32_t *lab_out, int amode, const AccTarget &at) {
@@ -559,6 +561,7 @@ __device__ __forceinline__ void resolve_lane(
   const bool sane = (xn < 1e18f) && (xn * cm < 1e30f) && (b1 < 1e30f);
   int bi = i1;
   if (!(sane && b2 - b1 > 2.0f * B)) {
+    if constexpr (STAGE1_ONLY) return false;
     const float lim = b1 + 2.0f * B;
     double best = INFINITY;
     bi = -1;
@@ -574,9 +577,9 @@ __device__ __forceinline__ void resolve_lane(
     }
   }
   lab_out[i] = bi;
-  if (!(amode & AM_ON)) return;
+  if (!(amode & AM_ON)) return true;
   const bool delta = amode & AM_DELTA;
-  if (delta && bi == prev) return;
+  if (delta && bi == prev) return true;
   const bool sub = delta && prev >= 0;
   for (int t = 0; t < d; ++t) {
     const double x = ld_x(xr + t);
@@ -585,6 +588,7 @@ __device__ __forceinline__ void resolve_lane(
   }
   at.count(bi, 1.0);
   if (sub) at.count(prev, -1.0);
+  return true;
 }
 
 // One wave = NB blocks of 16 samples per step.  Lane l = (q = l >> 4,
@@ -830,8 +834,9 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
       auto score = [&](int cb, const f32x4 (&accv)[NB]) {
         const uint32_t ib = (uint32_t)((cb - g0) * 4);  // wave-uniform tag
         uint32_t tag[4];  // opaque SGPRs: one v_and_or_b32 per score
+        const uint32_t t0 = opaque_s32(ib);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) tag[i] = opaque_s32(ib + i);
+        for (int i = 0; i < 4; ++i) tag[i] = t0 + i;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -1117,6 +1122,9 @@ __global__ void __launch_bounds__(BLOCK)
   double *lds_acc =
       (double *)((char *)smem + round_up(((int64_t)k * dp + k) * 4, 8));
   __shared__ unsigned long long blk_count;
+  // per wave: samples stage 1 left undecided, resolved 64 at a time (a
+  // lone stage-2 lane would otherwise hold its whole wave for a second pass)
+  __shared__ int2 dlist[BLOCK / 64][128];
   if (threadIdx.x == 0) blk_count = 0;
   {
     const f32x4 *src = (const f32x4 *)v.c32;
@@ -1134,18 +1142,41 @@ __global__ void __launch_bounds__(BLOCK)
   const int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
   const int64_t nwv = (int64_t)gridDim.x * (BLOCK / 64);
   unsigned long long mine = 0;
+  int2 *dl = dlist[threadIdx.x >> 6];
+  int dcnt = 0;  // wave-uniform
+  auto stage2 = [&](int2 it) {
+    resolve_lane<MAXD, VEC, TX>(X, ldx, d, k, base + it.x, it.y, cl, cnl, dp,
+                                cm, v.ct64, lab_out, amode, at);
+  };
   for (int64_t sg = wv; sg < nseg; sg += nwv) {
     const int cnt = v.tcount[sg];
     mine += cnt;
     const int2 *e = v.tlist + sg * TL_CAP;
     for (int t0 = 0; t0 < cnt; t0 += 64) {
+      int2 it = make_int2(0, 0);
+      bool ok = true;
       if (t0 + lane < cnt) {
-        const int2 it = e[t0 + lane];
-        resolve_lane<MAXD, VEC, TX>(X, ldx, d, k, base + it.x, it.y, cl, cnl,
-                                    dp, cm, v.ct64, lab_out, amode, at);
+        it = e[t0 + lane];
+        ok = resolve_lane<MAXD, VEC, TX, true>(X, ldx, d, k, base + it.x,
+                                               it.y, cl, cnl, dp, cm, v.ct64,
+                                               lab_out, amode, at);
+      }
+      const unsigned long long m = __ballot(!ok);
+      if (!ok) dl[dcnt + __popcll(m & ((1ull << lane) - 1))] = it;
+      dcnt += __popcll(m);
+      if (dcnt >= 64) {
+        wave_lds_sync();
+        stage2(dl[lane]);
+        const int rem = dcnt - 64;
+        const int2 tail = lane < rem ? dl[64 + lane] : make_int2(0, 0);
+        wave_lds_sync();
+        if (lane < rem) dl[lane] = tail;
+        dcnt = rem;
       }
     }
   }
+  wave_lds_sync();
+  if (lane < dcnt) stage2(dl[lane]);
   recheck_finish_count(mine, &blk_count, v);
   if (amode & AM_INLDS) flush_lds_acc(lds_acc, acc, k, d);
 }

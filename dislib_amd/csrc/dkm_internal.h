@@ -58,7 +58,7 @@ struct WsView {
 // Per-wave lists of the screen's undecided samples (resolved by
 // k_recheck_list without scanning the labels): one segment of TL_CAP
 // entries per screen wave, TL_SEGS >= 256 CUs x 32 waves.
-constexpr int TL_CAP = 256;
+constexpr int TL_CAP = 1024;
 constexpr int TL_SEGS = 8192;
 
 // MFMA fragment tiling of the centres: 16 centres x 16 dims per 1 KB block.
