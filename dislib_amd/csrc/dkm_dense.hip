@@ -531,25 +531,47 @@ __device__ __forceinline__ bool resolve_lane(
       xx = fmaf(xf[8 * b + m], xf[8 * b + m], xx);
     }
   }
-  // fp32 score of centre jc: fma chain over features (padding adds 0 * 0)
+  // fp32 score of centre jc: fma chain over features (padding adds 0 * 0).
+  // cl / cnl are the workspace's global fp32 centres, read through the
+  // constant address space: jc is wave-uniform, so the rows arrive by scalar
+  // loads into SGPRs (an LDS broadcast of the same row costs the full LDS
+  // return bandwidth, twice the VALU time of the fma chain).
+  typedef const __attribute__((address_space(4))) float cfloat;
+  typedef const __attribute__((address_space(4))) f32x4 cf32x4;
+  cfloat *clc = (cfloat *)cl;
+  cfloat *cnc = (cfloat *)cnl;
+  // full rows (dp == MAXD): no per-chunk branch, so the row's scalar loads
+  // issue together (one wait instead of one per 4 features)
+  const bool full = dp == MAXD;
   auto score = [&](int jc) {
-    const float *cr = cl + (int64_t)jc * dp;
+    cfloat *cr = clc + (int64_t)jc * dp;
     float dot = 0.f;
+    if (full) {
 #pragma unroll
-    for (int t4 = 0; t4 < MAXD / 4; ++t4) {
-      if (4 * t4 < dp) {
-        const f32x4 c4 = *(const f32x4 *)(cr + 4 * t4);
+      for (int t4 = 0; t4 < MAXD / 4; ++t4) {
+        const f32x4 c4 = *(cf32x4 *)(cr + 4 * t4);
         dot = fmaf(xf[4 * t4 + 0], c4.x, dot);
         dot = fmaf(xf[4 * t4 + 1], c4.y, dot);
         dot = fmaf(xf[4 * t4 + 2], c4.z, dot);
         dot = fmaf(xf[4 * t4 + 3], c4.w, dot);
       }
+    } else {
+#pragma unroll
+      for (int t4 = 0; t4 < MAXD / 4; ++t4) {
+        if (4 * t4 < dp) {
+          const f32x4 c4 = *(cf32x4 *)(cr + 4 * t4);
+          dot = fmaf(xf[4 * t4 + 0], c4.x, dot);
+          dot = fmaf(xf[4 * t4 + 1], c4.y, dot);
+          dot = fmaf(xf[4 * t4 + 2], c4.z, dot);
+          dot = fmaf(xf[4 * t4 + 3], c4.w, dot);
+        }
+      }
     }
-    return fmaf(-2.f, dot, cnl[jc]);
+    return fmaf(-2.f, dot, cnc[jc]);
   };
   float b1 = INFINITY, b2 = INFINITY;
   int i1 = 0;
-#pragma unroll 1
+#pragma unroll 2
   for (int jc = 0; jc < k; ++jc) {
     const float sc = score(jc);
     i1 = sc < b1 ? jc : i1;
@@ -603,26 +625,38 @@ __device__ __forceinline__ bool resolve_lane(
 // two xor-shuffles merge the four lanes of a sample.  lab_out[si] = label,
 // or -(prev + 2) when the screen cannot decide (the re-check resolves it;
 // prev = -1 outside AM_DELTA).
-template <int PREC, int NKS, int NB, bool VEC, class TX>
+//
+// CHUNK (k x d too large for LDS, e.g. k = 1000, d = 64): the fragments pass
+// through LDS in chunks of chb 16-centre blocks for every block step; the
+// sample loop is block-uniform (waves past n compute on zero rows and write
+// nothing) so that every wave reaches the chunk barriers.  L2 -> LDS traffic
+// per block step = all fragments (k * dpad * 4 B) per 16 * NB * SB/64 rows.
+template <int PREC, int NKS, int NB, bool VEC, class TX, bool CHUNK>
 __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
     k_screen(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
              WsView v, int32_t *__restrict__ lab_out, double *acc, int amode,
-             int64_t base, int use_list) {
+             int64_t base, int use_list, int chb) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int nkb = (int)(kpad16(k) / 16);
-  // fragment region: nkb*NKS blocks of 2 KB (f32: 8 floats per lane;
+  const int lkb = CHUNK ? chb : nkb;  // blocks resident in LDS at a time
+  // fragment region: lkb*NKS blocks of 2 KB (f32: 8 floats per lane;
   // bf16x3: 8 hi + 8 lo bf16 per lane)
   char *frag = (char *)smem;
-  float *cn = (float *)(frag + (int64_t)nkb * NKS * 2048);  // nkb*16
-  double *lds_acc = (double *)(cn + nkb * 16);
-  {
-    const f32x4 *src = (const f32x4 *)(PREC == P_F32 ? (const void *)v.cfrag
-                                                     : (const void *)v.bfrag);
+  float *cn = (float *)(frag + (int64_t)lkb * NKS * 2048);  // lkb*16
+  double *lds_acc = (double *)(cn + lkb * 16);
+  const f32x4 *fsrc = (const f32x4 *)(PREC == P_F32 ? (const void *)v.cfrag
+                                                    : (const void *)v.bfrag);
+  // LDS <- fragment blocks [c0, c1)
+  auto load_chunk = [&](int c0, int c1) {
+    const f32x4 *src = fsrc + (int64_t)c0 * NKS * 128;
     f32x4 *dst = (f32x4 *)frag;
-    for (int e = threadIdx.x; e < nkb * NKS * 128; e += SB) dst[e] = src[e];
-    for (int e = threadIdx.x; e < nkb * 16; e += SB) cn[e] = v.cnpad[e];
-    if (amode & AM_INLDS) zero_lds_acc(lds_acc, k, d);
-  }
+    for (int e = threadIdx.x; e < (c1 - c0) * NKS * 128; e += SB)
+      dst[e] = src[e];
+    for (int e = threadIdx.x; e < (c1 - c0) * 16; e += SB)
+      cn[e] = v.cnpad[c0 * 16 + e];
+  };
+  if (!CHUNK) load_chunk(0, nkb);
+  if (amode & AM_INLDS) zero_lds_acc(lds_acc, k, d);
   const float cm =
       (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
   const BoundK bk = bound_consts<PREC>(d, cm);
@@ -658,14 +692,14 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
                             (uint32_t)(8 * q * sizeof(TX));
   auto load_tile = [&](int64_t s0) {
     if (VEC && off32) {
-      const int64_t rows = n - s0;
+      const int64_t rows = std::max<int64_t>(0, n - s0);
       const int64_t xb = rows * ldx * (int64_t)sizeof(TX);
       const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)(X + s0 * ldx), 0,
+          (void *)(X + std::min(s0, n) * ldx), 0,
           (int)std::min<int64_t>(xb, 0x7fffffff), 0x00020000);
       if (delta) {
         const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(lab_out + s0), 0,
+            (void *)(lab_out + std::min(s0, n)), 0,
             (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
 #pragma unroll
         for (int b = 0; b < NB; ++b)
@@ -720,9 +754,12 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
     }
   };
 
+  // CHUNK: iterate on the block's first row so the trip count is
+  // block-uniform (every wave reaches the chunk barriers)
+  const int64_t wofs = (int64_t)wid * 16 * NB;
   int64_t s0 = base + wv * 16 * NB;
   if (s0 < n) load_tile(s0);
-  for (; s0 < n; s0 += step) {
+  for (; (CHUNK ? s0 - wofs : s0) < n; s0 += step) {
     // ---- convert the tile (fp64 -> fp32 -> operands), |x|^2 in fp32 ----
     float xx[NB];
     float xf[PREC == P_F32 ? NB : 1][NKS][8];
@@ -783,11 +820,12 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
     // MFMA chain of centre block cb into accv[], started from |c|^2; consumed
     // one chain later so that the next block's MFMAs overlap this block's
     // VALU scoring.
+    int cbase = 0;  // first LDS-resident block (CHUNK)
     auto chain = [&](int cb, f32x4 (&accv)[NB]) {
-      const f32x4 c4 = *(const f32x4 *)(cn + cb * 16 + 4 * q);
+      const f32x4 c4 = *(const f32x4 *)(cn + (cb - cbase) * 16 + 4 * q);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        const char *blk = frag + ((int64_t)cb * NKS + ks) * 2048;
+        const char *blk = frag + ((int64_t)(cb - cbase) * NKS + ks) * 2048;
         if constexpr (PREC == P_F32) {
           const f32x4 a0 = *(const f32x4 *)(blk + lane * 32);
           const f32x4 a1 = *(const f32x4 *)(blk + lane * 32 + 16);
@@ -823,8 +861,16 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
       r2[b] = 1e20f;
     }
 #else
-    for (int g0 = 0; g0 < nkb; g0 += GROUP_BLOCKS) {
-      const int g1 = min(nkb, g0 + GROUP_BLOCKS);
+    for (int c0 = 0; c0 < nkb; c0 += lkb) {
+    const int c1 = min(nkb, c0 + lkb);
+    if (CHUNK) {
+      __syncthreads();  // every wave is done with the previous chunk
+      load_chunk(c0, c1);
+      __syncthreads();
+    }
+    cbase = c0;
+    for (int g0 = c0; g0 < c1; g0 += GROUP_BLOCKS) {
+      const int g1 = min(c1, g0 + GROUP_BLOCKS);
       float b1[NB], b2[NB];  // packed, this group
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
@@ -872,6 +918,7 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
         r1[b] = nw ? b1[b] : r1[b];
       }
     }
+    }  // chunks
 #endif
     // merge the top-2 of the four lanes of a sample
     // (symmetric in the pair: both lanes get the same result whichever
@@ -1011,10 +1058,8 @@ __device__ __forceinline__ void recheck_finish_count(
 
 constexpr int RL_CAP = 128;  // per-wave list: a full batch + one chunk
 
-static size_t recheck_lane_lds(int64_t k, int64_t d) {
-  const int64_t dp = round_up(d, 4);
-  return (size_t)round_up((k * dp + k) * 4, 8) +
-         (size_t)(BLOCK / 64) * RL_CAP * 8;
+static size_t recheck_lane_lds(int64_t, int64_t) {
+  return (size_t)(BLOCK / 64) * RL_CAP * 8;
 }
 
 template <int MAXD, bool VEC, class TX>
@@ -1025,20 +1070,11 @@ __global__ void __launch_bounds__(BLOCK)
   if (v.hdr->qcount == 0) return;  // the screen resolved everything
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int dp = (int)round_up(d, 4);  // c32 row stride (dkm_util)
-  float *cl = (float *)smem;           // fp32 centres, k x dp (zero padded)
-  float *cnl = cl + (int64_t)k * dp;   // |c|^2 fp32
-  int64_t *lists =
-      (int64_t *)((char *)smem + round_up(((int64_t)k * dp + k) * 4, 8));
+  // (fp32 centres: global, scalar loads in resolve_lane)
+  int64_t *lists = (int64_t *)smem;
   double *lds_acc = (double *)(lists + (BLOCK / 64) * RL_CAP);
   __shared__ unsigned long long blk_count;
   if (threadIdx.x == 0) blk_count = 0;
-  {
-    const f32x4 *src = (const f32x4 *)v.c32;
-    f32x4 *dst = (f32x4 *)cl;
-    for (int64_t e = threadIdx.x; e < (int64_t)k * dp / 4; e += BLOCK)
-      dst[e] = src[e];
-    for (int e = threadIdx.x; e < k; e += BLOCK) cnl[e] = v.cn32[e];
-  }
   if (amode & AM_INLDS) zero_lds_acc(lds_acc, k, d);
   const float cm =
       (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
@@ -1049,7 +1085,8 @@ __global__ void __launch_bounds__(BLOCK)
   int64_t *wl = lists + (threadIdx.x >> 6) * RL_CAP;
 
   auto resolve = [&](int64_t i) {
-    resolve_lane<MAXD, VEC, TX>(X, ldx, d, k, i, -lab_out[i] - 2, cl, cnl, dp,
+    resolve_lane<MAXD, VEC, TX>(X, ldx, d, k, i, -lab_out[i] - 2, v.c32,
+                                v.cn32, dp,
                                 cm, v.ct64, lab_out, amode, at);
   };
 
@@ -1117,22 +1154,13 @@ __global__ void __launch_bounds__(BLOCK)
                    int amode, int64_t base, int nseg) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int dp = (int)round_up(d, 4);
-  float *cl = (float *)smem;           // fp32 centres, k x dp (zero padded)
-  float *cnl = cl + (int64_t)k * dp;   // |c|^2 fp32
-  double *lds_acc =
-      (double *)((char *)smem + round_up(((int64_t)k * dp + k) * 4, 8));
+  // (fp32 centres: global, scalar loads in resolve_lane)
+  double *lds_acc = (double *)smem;
   __shared__ unsigned long long blk_count;
   // per wave: samples stage 1 left undecided, resolved 64 at a time (a
   // lone stage-2 lane would otherwise hold its whole wave for a second pass)
   __shared__ int2 dlist[BLOCK / 64][128];
   if (threadIdx.x == 0) blk_count = 0;
-  {
-    const f32x4 *src = (const f32x4 *)v.c32;
-    f32x4 *dst = (f32x4 *)cl;
-    for (int64_t e = threadIdx.x; e < (int64_t)k * dp / 4; e += BLOCK)
-      dst[e] = src[e];
-    for (int e = threadIdx.x; e < k; e += BLOCK) cnl[e] = v.cn32[e];
-  }
   if (amode & AM_INLDS) zero_lds_acc(lds_acc, k, d);
   const float cm =
       (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
@@ -1145,7 +1173,8 @@ __global__ void __launch_bounds__(BLOCK)
   int2 *dl = dlist[threadIdx.x >> 6];
   int dcnt = 0;  // wave-uniform
   auto stage2 = [&](int2 it) {
-    resolve_lane<MAXD, VEC, TX>(X, ldx, d, k, base + it.x, it.y, cl, cnl, dp,
+    resolve_lane<MAXD, VEC, TX>(X, ldx, d, k, base + it.x, it.y, v.c32,
+                                v.cn32, dp,
                                 cm, v.ct64, lab_out, amode, at);
   };
   for (int64_t sg = wv; sg < nseg; sg += nwv) {
@@ -1158,7 +1187,8 @@ __global__ void __launch_bounds__(BLOCK)
       if (t0 + lane < cnt) {
         it = e[t0 + lane];
         ok = resolve_lane<MAXD, VEC, TX, true>(X, ldx, d, k, base + it.x,
-                                               it.y, cl, cnl, dp, cm, v.ct64,
+                                               it.y, v.c32, v.cn32, dp, cm,
+                                               v.ct64,
                                                lab_out, amode, at);
       }
       const unsigned long long m = __ballot(!ok);
@@ -1301,25 +1331,31 @@ static size_t screen_lds_fixed(int64_t k, int64_t d) {
   return (size_t)(kpad16(k) * dpad32(d) * 4 + kpad16(k) * 4);
 }
 
+// Larger k x d runs the CHUNK screen (fragments staged through LDS).
 static bool screen_ok(int64_t k, int64_t d) {
-  return k >= 2 && k <= 32767 && d <= 128 &&
-         screen_lds_fixed(k, d) <= LDS_BUDGET;
+  return k >= 2 && k <= 32767 && d <= 128;
 }
 
-template <int PREC, int NKS, int NB, bool VEC, class TX>
+// 16-centre blocks resident in LDS per chunk (CHUNK screen), 0 = all fit
+static int screen_chunk_blocks(int64_t k, int64_t d) {
+  if (screen_lds_fixed(k, d) <= LDS_BUDGET) return 0;
+  const int64_t per = (dpad32(d) / 32) * 2048 + 64;
+  return (int)std::max<int64_t>(1, (int64_t)LDS_BUDGET / per);
+}
+
+template <int PREC, int NKS, int NB, bool VEC, class TX, bool CHUNK>
 static int launch_screen_t(const TX *X, int64_t end, int d, int64_t ldx,
                            int k, const WsView &v, int32_t *lab_out,
                            double *acc, int amode, int64_t base, size_t lds,
-                           int use_list, hipStream_t s, int *nseg) {
-  const void *kf = (const void *)k_screen<PREC, NKS, NB, VEC, TX>;
+                           int use_list, int chb, hipStream_t s, int *nseg) {
+  const void *kf = (const void *)k_screen<PREC, NKS, NB, VEC, TX, CHUNK>;
   const int64_t cap = (int64_t)dev_info().cus * resident_blocks(kf, SB, lds);
   const int64_t per_block = 16 * NB * (SB / 64);
   const int64_t need = (end - base + per_block - 1) / per_block;
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min(need, cap));
   *nseg = (int)std::min<int64_t>((int64_t)g * (SB / 64), TL_SEGS);
-  k_screen<PREC, NKS, NB, VEC, TX><<<g, SB, lds, s>>>(X, end, d, ldx, k, v,
-                                                      lab_out, acc, amode,
-                                                      base, use_list);
+  k_screen<PREC, NKS, NB, VEC, TX, CHUNK><<<g, SB, lds, s>>>(
+      X, end, d, ldx, k, v, lab_out, acc, amode, base, use_list, chb);
   return check_launch("screen assignment");
 }
 
@@ -1327,12 +1363,16 @@ template <int PREC, bool VEC, class TX>
 static int launch_screen_nks(const TX *X, int64_t end, int d, int64_t ldx,
                              int k, const WsView &v, int32_t *lab_out,
                              double *acc, int amode, int64_t base, size_t lds,
-                             int use_list, hipStream_t s, int *nseg) {
+                             int use_list, int chb, hipStream_t s,
+                             int *nseg) {
 #define DKM_SCREEN_CASE(NKS, NB)                                             \
   case NKS:                                                                  \
-    return launch_screen_t<PREC, NKS, NB, VEC, TX>(X, end, d, ldx, k, v,     \
-                                                   lab_out, acc, amode, base, \
-                                                   lds, use_list, s, nseg);
+    return chb ? launch_screen_t<PREC, NKS, NB, VEC, TX, true>(              \
+                     X, end, d, ldx, k, v, lab_out, acc, amode, base, lds,   \
+                     use_list, chb, s, nseg)                                 \
+               : launch_screen_t<PREC, NKS, NB, VEC, TX, false>(             \
+                     X, end, d, ldx, k, v, lab_out, acc, amode, base, lds,   \
+                     use_list, chb, s, nseg);
   switch (dpad32(d) / 32) {
     DKM_SCREEN_CASE(1, DKM_NB1)
     DKM_SCREEN_CASE(2, 1)
@@ -1432,7 +1472,7 @@ static int launch_list(const TX *X, int d, int64_t ldx, int k,
                        const WsView &v, int32_t *lab_out, double *acc,
                        int acc_kind, bool vec, int64_t base, int nseg,
                        hipStream_t s) {
-  const size_t fb = (size_t)round_up(((int64_t)k * round_up(d, 4) + k) * 4, 8);
+  const size_t fb = 0;  // centres are read from global (scalar loads)
   const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
   const int amode = acc_mode(acc_kind, fb + a_bytes <= LDS_BUDGET);
   const size_t lds = fb + ((amode & AM_INLDS) ? a_bytes : 0);
@@ -1445,6 +1485,115 @@ static int launch_list(const TX *X, int d, int64_t ldx, int k,
   const int r = maxd == 32 ? DKM_LL(32) : maxd == 64 ? DKM_LL(64) : DKM_LL(128);
 #undef DKM_LL
   return r;
+}
+
+
+// ---------------------------------------------------------------------------
+// Label-partitioned sums (k x d sums too large for block-private LDS, e.g.
+// k = 1000, d = 64: 512 KB).  Instead of d fp64 global atomics per sample
+// (8e9 of them at 125M x 64: ~0.5 s), block (x, y) owns the clusters
+// [y*kr, y*kr + kr) -- their sums fit in LDS -- and the sample range of its
+// waves; every row is read (coalesced, lanes over features) only by the
+// blocks whose cluster range holds its label, so X is read once in all.
+// Labels are read gridDim.y times (4 B each).  Delta (prev != null): only
+// samples whose label changed, +x to the new cluster and -x from the old.
+// The block's LDS sums are flushed once with fp64 atomics.
+// ---------------------------------------------------------------------------
+template <class TX>
+__global__ void __launch_bounds__(BLOCK)
+    k_label_sums(const TX *__restrict__ X, int64_t lo, int64_t hi, int d,
+                 int64_t ldx, const int32_t *__restrict__ lab,
+                 const int32_t *__restrict__ prev, int k, int kr,
+                 double *acc) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int c0 = blockIdx.y * kr, c1 = min(k, c0 + kr), nc = c1 - c0;
+  const int ds = lds_stride(d);
+  double *rows = smem;
+  double *cnt = smem + (int64_t)nc * ds;
+  for (int64_t e = threadIdx.x; e < (int64_t)nc * ds + nc; e += BLOCK)
+    smem[e] = 0.0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+  const int64_t nwv = (int64_t)gridDim.x * (BLOCK / 64);
+  for (int64_t i0 = lo + wv * 64; i0 < hi; i0 += nwv * 64) {
+    const int64_t i = i0 + lane;
+    int a = -1, p = -1;
+    if (i < hi) {
+      a = lab[i];
+      if (prev) {
+        p = prev[i];
+        if (p == a) a = p = -1;
+      }
+    }
+    const bool ina = a >= c0 && a < c1, inp = p >= c0 && p < c1;
+    uint64_t m = __ballot(ina || inp);
+    while (m) {  // wave-uniform: 4 rows per pass, loads issued together
+      int bl[4], ua[4], up[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        bl[u] = m ? __builtin_ctzll(m) : -1;
+        if (m) m &= m - 1;
+        ua[u] = bl[u] >= 0 ? __builtin_amdgcn_readlane(a, bl[u]) : -1;
+        up[u] = bl[u] >= 0 ? __builtin_amdgcn_readlane(p, bl[u]) : -1;
+      }
+      for (int t = lane; t < d; t += 64) {
+        double x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          x[u] = bl[u] >= 0 ? ld_x(X + (i0 + bl[u]) * ldx + t) : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (ua[u] >= c0 && ua[u] < c1)
+            lds_add(rows + (int64_t)(ua[u] - c0) * ds + t, x[u]);
+          if (up[u] >= c0 && up[u] < c1)
+            lds_add(rows + (int64_t)(up[u] - c0) * ds + t, -x[u]);
+        }
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (ua[u] >= c0 && ua[u] < c1) lds_add(cnt + (ua[u] - c0), 1.0);
+          if (up[u] >= c0 && up[u] < c1) lds_add(cnt + (up[u] - c0), -1.0);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t nd = (int64_t)nc * d;
+  for (int64_t e = threadIdx.x; e < nd + nc; e += BLOCK) {
+    const double v = e < nd ? rows[(e / d) * ds + (e % d)] : cnt[e - nd];
+    if (v != 0.0)
+      atomic_add_f64(e < nd ? acc + (int64_t)c0 * d + e
+                            : acc + (int64_t)k * d + c0 + (e - nd),
+                     v);
+  }
+}
+
+// Clusters per k_label_sums range: their LDS sums within LDS_BUDGET.
+static int label_sums_kr(int64_t k, int d) {
+  const int64_t per = ((int64_t)lds_stride(d) + 1) * 8;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(k, LDS_BUDGET / per));
+}
+
+template <class TX>
+static int launch_label_sums(const TX *X, int64_t lo, int64_t hi, int d,
+                             int64_t ldx, const int32_t *lab,
+                             const int32_t *prev, int k, double *acc,
+                             hipStream_t s) {
+  if (hi <= lo) return 0;
+  const int kr = label_sums_kr(k, d);
+  const int ny = (k + kr - 1) / kr;
+  const size_t lds = (size_t)(((int64_t)lds_stride(d) + 1) * kr) * 8;
+  const void *kf = (const void *)k_label_sums<TX>;
+  const int64_t cap = (int64_t)dev_info().cus * resident_blocks(kf, BLOCK, lds);
+  const int64_t waves = (hi - lo + 63) / 64;
+  const int64_t gx = std::max<int64_t>(
+      1, std::min<int64_t>((cap + ny - 1) / ny * 2,
+                           (waves + BLOCK / 64 - 1) / (BLOCK / 64)));
+  k_label_sums<TX><<<dim3((unsigned)gx, (unsigned)ny), BLOCK, lds, s>>>(
+      X, lo, hi, d, ldx, lab, prev, k, kr, acc);
+  return check_launch("label sums");
 }
 
 // Screen + exact re-check over [0, n).  Labels go to `labels` when given,
@@ -1460,9 +1609,25 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   if (!labels && nq < 1)
     return fail(DKM_E_WORKSPACE, "screen: no label scratch");
   const int64_t chunk = labels ? n : nq;
-  const size_t fb = screen_lds_fixed(k, d);
+  const int chb = screen_chunk_blocks(k, d);
+  const size_t fb =
+      chb ? (size_t)chb * ((dpad32(d) / 32) * 2048 + 64) : screen_lds_fixed(k, d);
   const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
-  const int amode = acc_mode(acc_kind, fb + a_bytes <= LDS_BUDGET);
+  // sums that do not fit block-private LDS: the screen writes labels only
+  // and k_label_sums accumulates from them (delta: against a copy of the
+  // previous labels in the label scratch)
+  const bool lds_fits = fb + a_bytes <= LDS_BUDGET;
+  const bool post = acc_kind != 0 && !lds_fits && !getenv("DKM_NO_POST") &&
+                    (acc_kind == 1 || (labels && nq >= n));
+  const int32_t *prevbuf = nullptr;
+  if (post && acc_kind == 2) {
+    if (hipMemcpyAsync(v.queue, labels, (size_t)n * 4,
+                       hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return fail(DKM_E_LAUNCH, "screen: label copy");
+    prevbuf = v.queue;
+  }
+  const int skind = post ? 0 : acc_kind;
+  const int amode = acc_mode(skind, lds_fits);
   const size_t lds = fb + ((amode & AM_INLDS) ? a_bytes : 0);
   const bool vec = (d % 8 == 0) && (ldx % (16 / (int64_t)sizeof(TX)) == 0) &&
                    (((uintptr_t)X % 16) == 0);
@@ -1474,23 +1639,26 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
     if (prec == P_F32)
       r = vec ? launch_screen_nks<P_F32, true, TX>(X, end, d, ldx, k, v,
                                                    lab_out, acc, amode, base,
-                                                   lds, use_list, s, &nseg)
+                                                   lds, use_list, chb, s, &nseg)
               : launch_screen_nks<P_F32, false, TX>(X, end, d, ldx, k, v,
                                                     lab_out, acc, amode, base,
-                                                    lds, use_list, s, &nseg);
+                                                    lds, use_list, chb, s, &nseg);
     else
       r = vec ? launch_screen_nks<P_B3, true, TX>(X, end, d, ldx, k, v,
                                                   lab_out, acc, amode, base,
-                                                  lds, use_list, s, &nseg)
+                                                  lds, use_list, chb, s, &nseg)
               : launch_screen_nks<P_B3, false, TX>(X, end, d, ldx, k, v,
                                                    lab_out, acc, amode, base,
-                                                   lds, use_list, s, &nseg);
+                                                   lds, use_list, chb, s, &nseg);
     if (r) return r;
     if (use_list && (r = launch_list<TX>(X, d, ldx, k, v, lab_out, acc,
-                                         acc_kind, vec, base, nseg, s)))
+                                         skind, vec, base, nseg, s)))
       return r;
     if ((r = launch_recheck<TX>(X, end, d, ldx, k, v, lab_out, acc,
-                                acc_kind, vec, base, s)))
+                                skind, vec, base, s)))
+      return r;
+    if (post && (r = launch_label_sums<TX>(X, base, end, d, ldx, lab_out,
+                                           prevbuf, k, acc, s)))
       return r;
   }
   return 0;

@@ -249,7 +249,11 @@ def _partial_sum_gpu(x, C, mode):
     (2000, 100, 12, 7), (1000, 129, 8, 8), (600, 300, 5, 9),
     (257, 1024, 33, 10), (4097, 1, 2, 11), (70, 3, 1, 12),
     (3000, 32, 300, 13), (3000, 16, 250, 14), (2000, 100, 193, 15),
-    (2000, 32, 600, 16)])
+    (2000, 32, 600, 16),
+    # fragments larger than LDS: the CHUNK screen (k x d staged in chunks;
+    # d = 33 unaligned rows; k = 5000: several chunks and packing groups)
+    (3000, 64, 1000, 17), (2000, 128, 700, 18), (3000, 33, 1500, 19),
+    (6000, 16, 5000, 20)])
 def test_partial_sum_vs_oracle(mode, n, d, k, seed):
     rng = np.random.default_rng(seed)
     x = rng.standard_normal((n, d)) * rng.uniform(0.5, 20)
@@ -372,7 +376,7 @@ def test_large_fit_properties():
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("d,k", [(32, 100), (7, 5), (64, 40), (16, 300),
-                                 (130, 9)])
+                                 (130, 9), (64, 1000)])
 def test_assign_delta_equals_difference_of_partial_sums(mode, d, k):
     from dislib_amd import _device, _lib
     rng = np.random.default_rng(d * 100 + k)
@@ -437,14 +441,14 @@ def test_fit_delta_refresh_matches_oracle(refresh):
 
 
 @pytest.mark.parametrize("mode", ["screen32", "bf16x3"])
-def test_screen_stress_vs_exact_kernel(mode):
+@pytest.mark.parametrize("n,d,k", [(1_000_000, 32, 100), (200_000, 64, 1000)])
+def test_screen_stress_vs_exact_kernel(mode, n, d, k):
     """1M samples x 2 repetitions against the exact kernel on the same
     (fitted) centres: a timing hazard or race that corrupts a handful of
     labels per million shows up here (the exact kernel itself is pinned to
     the oracle by the tests above)."""
     from dislib_amd import _device, _lib
     from dislib_amd.data import Dataset, Subset
-    n, d, k = 1_000_000, 32, 100
     X = torch.empty((n, d), dtype=torch.float64, device="cuda")
     _device.make_blobs(X, 0, k, seed=3)
     ds = Dataset(n_features=d)
