@@ -374,6 +374,11 @@ __device__ __forceinline__ uint32_t opaque_s32(uint32_t v) {
   asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "s"(v));
   return r;
 }
+// set bits of a wave mask below this lane (v_mbcnt: no 64-bit lane mask)
+__device__ __forceinline__ int lane_prefix(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi(
+      (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 // min without fminf's NaN canonicalisation: the screen's NaN/Inf samples
 // are caught by its `sane` test either way.  ninf = opaque -inf.
 __device__ __forceinline__ float min_nc(float a, float b, float ninf) {
@@ -426,6 +431,18 @@ __device__ __forceinline__ BoundK bound_consts(int d, float cm) {
   k.cm = cm;
   // v_sqrt_f32 (<= 1 ulp) instead of the correctly rounded sqrtf: 4 more ulp
   k.xn_scale = 1.0f + (d + 8) * 0x1.0p-24f;
+  // wave-uniform: keep them in SGPRs (in VGPRs they were spilled, and the
+  // reload's vmcnt(0) waited for the prefetched tile)
+  auto u = [](float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+  };
+  k.k_mag = u(k.k_mag);
+  k.k_s2 = u(k.k_s2);
+  k.k_s1 = u(k.k_s1);
+  k.two_cm = u(k.two_cm);
+  k.cm2 = u(k.cm2);
+  k.cm = u(k.cm);
+  k.xn_scale = u(k.xn_scale);
   return k;
 }
 // 2B for a sample with fp32 |x|^2 = xx (packed scores)
@@ -958,7 +975,7 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
       const int add = __popcll(um);
       if (listing && tl_cnt + add <= TL_CAP) {
         if (q == 0 && und)
-          wl[tl_cnt + __popcll(um & ((1ull << lane) - 1))] =
+          wl[tl_cnt + lane_prefix(um)] =
               make_int2((int)(si - base), prev);
         tl_cnt += add;
       } else {
@@ -1000,6 +1017,266 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
       }
     }
     if (full_acc && s_next < n) load_tile(s_next);  // the tile was in use
+  }
+  if (lane == 0) {
+    if (listing) v.tcount[seg] = tl_cnt;
+    if (tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
+  }
+  if (amode & AM_INLDS) {
+    __syncthreads();
+    flush_lds_acc(lds_acc, acc, k, d);
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// bf16x3 screen on v_mfma_f32_32x32x16_bf16 for d <= 32 (16-B aligned rows):
+// one wave step = 32 samples (B columns) x 32-centre blocks (A rows).  Lane
+// l = (r = l & 31, h = l >> 5) holds the 16 contiguous features 16h..16h+15
+// of sample r (K-slice ks takes features 16h + 8ks + j, the same permuted K
+// order as the W32 fragments built by k_frag), so a sample's partial |x|^2
+// and top-2 need one permlane32 swap to merge, and every per-sample cost
+// (conversion, merge, bound, label, list) is paid by 2 lanes instead of the
+// 16x16 kernel's 4.  Accumulator register g holds centre
+// cb*32 + (g & 3) + 8 (g >> 2) + 4h; the packing tag is (block in group) x 16
+// + g, PACK_BITS = 7 -> groups of 8 blocks.  Same bound, same exactness
+// argument and the same list / label / accumulation contract as k_screen.
+// ---------------------------------------------------------------------------
+constexpr int SBW = 256;  // k_screen_w32 block: 4 waves, 3 blocks per CU
+template <class TX>
+__global__ void __launch_bounds__(SBW) __attribute__((amdgpu_waves_per_eu(3)))
+    k_screen_w32(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
+                 int k, WsView v, int32_t *__restrict__ lab_out, double *acc,
+                 int amode, int64_t base, int use_list) {
+  constexpr int GB = 8;  // 32-centre blocks per packing group
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nkb = (int)(kpad32(k) / 32);
+  char *frag = (char *)smem;                          // nkb x 4 KB
+  float *cn = (float *)(frag + (int64_t)nkb * 4096);  // nkb x 32
+  double *lds_acc = (double *)(cn + nkb * 32);
+  {
+    const f32x4 *src = (const f32x4 *)v.b32frag;
+    f32x4 *dst = (f32x4 *)frag;
+    for (int e = threadIdx.x; e < nkb * 256; e += SBW) dst[e] = src[e];
+    for (int e = threadIdx.x; e < nkb * 32; e += SBW) cn[e] = v.cn32f[e];
+  }
+  if (amode & AM_INLDS) zero_lds_acc(lds_acc, k, d);
+  const float cm =
+      (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
+  const BoundK bk = bound_consts<P_B3>(d, cm);
+  const float ninf = __uint_as_float(opaque_u32(0xff800000u));
+  const uint32_t vmask = opaque_u32(~PACK_MASK);
+  const bool full_acc = am_full(amode);
+  const bool delta = amode & AM_DELTA;
+  const AccTarget at = acc_target(amode, lds_acc, acc, k, d);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t wv = (int64_t)blockIdx.x * (SBW / 64) + wid;
+  const int64_t step = (int64_t)gridDim.x * (SBW / 64) * 32;
+  const int64_t seg = wv;
+  int2 *wl = v.tlist + seg * TL_CAP;
+  const bool listing = use_list && seg < TL_SEGS;
+  int tl_cnt = 0, tl_over = 0;
+
+  double tile[16];
+  int pv = -1;
+  const uint32_t lane_off = (uint32_t)(r * ldx * (int64_t)sizeof(TX)) +
+                            (uint32_t)(16 * h * sizeof(TX));
+  auto load_tile = [&](int64_t s0) {
+    const int64_t rows = std::max<int64_t>(0, n - s0);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(X + std::min(s0, n) * ldx), 0,
+        (int)std::min<int64_t>(rows * ldx * (int64_t)sizeof(TX), 0x7fffffff),
+        0x00020000);
+    if (delta) {
+      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(lab_out + std::min(s0, n)), 0,
+          (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
+      pv = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if (16 * h + 8 * ks < d) {
+        // one lane offset register; the constant part rides in soffset
+        const int o = 8 * ks * (int)sizeof(TX);
+        if constexpr (sizeof(TX) == 8) {
+#pragma unroll
+          for (int p4 = 0; p4 < 4; ++p4) {
+            const double2 v2 = __builtin_bit_cast(
+                double2, __builtin_amdgcn_raw_buffer_load_b128(
+                             rx, lane_off, o + 16 * p4, 0));
+            tile[8 * ks + 2 * p4] = v2.x;
+            tile[8 * ks + 2 * p4 + 1] = v2.y;
+          }
+        } else {
+#pragma unroll
+          for (int p4 = 0; p4 < 2; ++p4) {
+            const float4 v4 = __builtin_bit_cast(
+                float4, __builtin_amdgcn_raw_buffer_load_b128(
+                            rx, lane_off, o + 16 * p4, 0));
+            tile[8 * ks + 4 * p4] = v4.x;
+            tile[8 * ks + 4 * p4 + 1] = v4.y;
+            tile[8 * ks + 4 * p4 + 2] = v4.z;
+            tile[8 * ks + 4 * p4 + 3] = v4.w;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) tile[8 * ks + m] = 0.0;
+      }
+    }
+  };
+
+  int64_t s0 = base + wv * 32;
+  if (s0 < n) load_tile(s0);
+  for (; s0 < n; s0 += step) {
+    float xx = 0.f;
+    bf16x8 xh[2], xl[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int m = 0; m < 8; m += 2) {
+        const float x0 = (float)tile[8 * ks + m];
+        const float x1 = (float)tile[8 * ks + m + 1];
+        xx = fmaf(x0, x0, xx);
+        xx = fmaf(x1, x1, xx);
+        const bf16x2 h2 = __builtin_convertvector(f32x2{x0, x1}, bf16x2);
+        const uint32_t hu = __builtin_bit_cast(uint32_t, h2);
+        const float h0 = __uint_as_float(hu << 16);
+        const float h1 = __uint_as_float(hu & 0xffff0000u);
+        const bf16x2 l2 =
+            __builtin_convertvector(f32x2{x0 - h0, x1 - h1}, bf16x2);
+        xh[ks][m] = h2[0];
+        xh[ks][m + 1] = h2[1];
+        xl[ks][m] = l2[0];
+        xl[ks][m + 1] = l2[1];
+      }
+    {
+      float xa, xb;
+      pair_xor<32>(xx, xa, xb);
+      xx = xa + xb;
+    }
+    const int prv = pv;
+    const int64_t s_next = s0 + step;
+    if (!full_acc && s_next < n) load_tile(s_next);
+
+    float r1 = INFINITY, r2 = INFINITY;
+    int ri = 0;
+    typedef float f32x16 __attribute__((ext_vector_type(16)));
+    auto chain = [&](int cb, f32x16 &accv) {
+      const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
+      const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
+      accv = f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                    c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const char *blk = frag + ((int64_t)cb * 2 + ks) * 2048;
+        const bf16x8 ah = *(const bf16x8 *)(blk + lane * 16);
+        const bf16x8 al = *(const bf16x8 *)(blk + 1024 + lane * 16);
+        accv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xh[ks], accv, 0, 0,
+                                                       0);
+        accv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xl[ks], accv, 0, 0,
+                                                       0);
+        accv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, xh[ks], accv, 0, 0,
+                                                       0);
+      }
+    };
+    for (int g0 = 0; g0 < nkb; g0 += GB) {
+      const int g1 = min(nkb, g0 + GB);
+      float b1 = INFINITY, b2 = INFINITY;
+      auto score = [&](int cb, const f32x16 &accv) {
+        const uint32_t t0 = opaque_s32((uint32_t)((cb - g0) * 16));
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const float sp =
+              __uint_as_float((__float_as_uint(accv[g]) & vmask) | (t0 + g));
+          b2 = __builtin_amdgcn_fmed3f(b1, b2, sp);
+          b1 = min_nc(b1, sp, ninf);
+        }
+      };
+      f32x16 acc_a, acc_b;
+      chain(g0, acc_a);
+      int cb = g0;
+      for (; cb + 2 <= g1; cb += 2) {
+        chain(cb + 1, acc_b);
+        score(cb, acc_a);
+        if (cb + 2 < g1) chain(cb + 2, acc_a);
+        score(cb + 1, acc_b);
+      }
+      if (cb < g1) score(cb, acc_a);
+      const uint32_t tg = __float_as_uint(b1) & PACK_MASK;
+      const int g = (int)(tg & 15);
+      const int gi = (g0 + (int)(tg >> 4)) * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+      const bool nw = b1 < r1;
+      r2 = nw ? min_nc(r1, b2, ninf) : min_nc(r2, b1, ninf);
+      ri = nw ? gi : ri;
+      r1 = nw ? b1 : r1;
+    }
+    {  // merge the two lanes of a sample (symmetric in the pair)
+      float a1, c1, a2, c2;
+      int ai, ci;
+      pair_xor<32>(r1, a1, c1);
+      pair_xor<32>(r2, a2, c2);
+      pair_xor<32>(ri, ai, ci);
+      const bool tc = (c1 < a1) | ((c1 == a1) & (ci < ai));
+      r1 = tc ? c1 : a1;
+      ri = tc ? ci : ai;
+      r2 = tc ? min_nc(a1, c2, ninf) : min_nc(a2, c1, ninf);
+    }
+    const int64_t si = s0 + r;
+    float xn;
+    const float B2 = bound2_fast(bk, xx, xn);
+    const bool sane = (xn < 1e18f) & (xn * cm < 1e30f) & (r1 < 1e30f);
+    const bool unique = sane & (r2 - r1 > B2);
+    const bool und = si < n && !unique;
+    const int prev = delta ? prv : -1;
+    const uint64_t um = __ballot(h == 0 && und);
+    const int add = __popcll(um);
+    if (listing && tl_cnt + add <= TL_CAP) {
+      if (h == 0 && und)
+        wl[tl_cnt + lane_prefix(um)] =
+            make_int2((int)(si - base), prev);
+      tl_cnt += add;
+    } else {
+      tl_over += add;
+    }
+    if (si < n) {
+      const int lab = ri;
+      if (h == 0 && !(unique && lab == prev))
+        lab_out[si] = unique ? lab : -(prev + 2);
+      if (unique) {
+        if (full_acc) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+              const int t = 16 * h + 8 * ks + m;
+              if (t < d) at.add(lab, t, tile[8 * ks + m]);
+            }
+          if (h == 0) at.count(lab, 1.0);
+        } else if (delta && lab != prev) {
+          const TX *xr = X + si * ldx;
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+              const int t = 16 * h + 8 * ks + m;
+              if (t < d) {
+                const double x = ld_x(xr + t);
+                at.add(lab, t, x);
+                if (prev >= 0) at.add(prev, t, -x);
+              }
+            }
+          if (h == 0) {
+            at.count(lab, 1.0);
+            if (prev >= 0) at.count(prev, -1.0);
+          }
+        }
+      }
+    }
+    if (full_acc && s_next < n) load_tile(s_next);
   }
   if (lane == 0) {
     if (listing) v.tcount[seg] = tl_cnt;
@@ -1359,6 +1636,22 @@ static int launch_screen_t(const TX *X, int64_t end, int d, int64_t ldx,
   return check_launch("screen assignment");
 }
 
+template <class TX>
+static int launch_screen_w32(const TX *X, int64_t end, int d, int64_t ldx,
+                             int k, const WsView &v, int32_t *lab_out,
+                             double *acc, int amode, int64_t base, size_t lds,
+                             int use_list, hipStream_t s, int *nseg) {
+  const void *kf = (const void *)k_screen_w32<TX>;
+  const int64_t cap = (int64_t)dev_info().cus * resident_blocks(kf, SBW, lds);
+  const int64_t per_block = 32 * (SBW / 64);
+  const int64_t need = (end - base + per_block - 1) / per_block;
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min(need, cap));
+  *nseg = (int)std::min<int64_t>((int64_t)g * (SBW / 64), TL_SEGS);
+  k_screen_w32<TX><<<g, SBW, lds, s>>>(X, end, d, ldx, k, v, lab_out, acc,
+                                      amode, base, use_list);
+  return check_launch("screen assignment (32x32)");
+}
+
 template <int PREC, bool VEC, class TX>
 static int launch_screen_nks(const TX *X, int64_t end, int d, int64_t ldx,
                              int k, const WsView &v, int32_t *lab_out,
@@ -1609,9 +1902,17 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   if (!labels && nq < 1)
     return fail(DKM_E_WORKSPACE, "screen: no label scratch");
   const int64_t chunk = labels ? n : nq;
-  const int chb = screen_chunk_blocks(k, d);
-  const size_t fb =
-      chb ? (size_t)chb * ((dpad32(d) / 32) * 2048 + 64) : screen_lds_fixed(k, d);
+  const bool vec = (d % 8 == 0) && (ldx % (16 / (int64_t)sizeof(TX)) == 0) &&
+                   (((uintptr_t)X % 16) == 0);
+  // d <= 32 bf16x3 with the 32x32x16 fragments resident: k_screen_w32
+  const size_t fb32 = (size_t)(kpad32(k) / 32) * (4096 + 128);
+  const bool w32 = prec == P_B3 && d <= 32 && vec && fb32 <= LDS_BUDGET &&
+                   (int64_t)32 * ldx * (int64_t)sizeof(TX) < (1ll << 31) &&
+                   !getenv("DKM_NO_W32");
+  const int chb = w32 ? 0 : screen_chunk_blocks(k, d);
+  const size_t fb = w32 ? fb32
+                    : chb ? (size_t)chb * ((dpad32(d) / 32) * 2048 + 64)
+                          : screen_lds_fixed(k, d);
   const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
   // sums that do not fit block-private LDS: the screen writes labels only
   // and k_label_sums accumulates from them (delta: against a copy of the
@@ -1629,14 +1930,15 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const int skind = post ? 0 : acc_kind;
   const int amode = acc_mode(skind, lds_fits);
   const size_t lds = fb + ((amode & AM_INLDS) ? a_bytes : 0);
-  const bool vec = (d % 8 == 0) && (ldx % (16 / (int64_t)sizeof(TX)) == 0) &&
-                   (((uintptr_t)X % 16) == 0);
   const int use_list = list_ok(k, d) && !getenv("DKM_NO_LIST") ? 1 : 0;
   for (int64_t base = 0; base < n; base += chunk) {
     const int64_t end = std::min(n, base + chunk);
     int32_t *lab_out = labels ? labels : v.queue - base;
     int r, nseg = 0;
-    if (prec == P_F32)
+    if (w32)
+      r = launch_screen_w32<TX>(X, end, d, ldx, k, v, lab_out, acc, amode,
+                                base, lds, use_list, s, &nseg);
+    else if (prec == P_F32)
       r = vec ? launch_screen_nks<P_F32, true, TX>(X, end, d, ldx, k, v,
                                                    lab_out, acc, amode, base,
                                                    lds, use_list, chb, s, &nseg)

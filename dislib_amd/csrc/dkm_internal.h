@@ -50,6 +50,8 @@ struct WsView {
   float *cfrag;   // fp32 -2*centres in MFMA A-fragment order (dkm_dense)
   float *cnpad;   // kpad16 fp32 ||c||^2, 2^100 for padding centres
   uint16_t *bfrag; // bf16 hi/lo of -2*centres, 16x16x32 fragment order
+  uint16_t *b32frag; // d <= 32: bf16 hi/lo, 32x32x16 order (k_screen_w32)
+  float *cn32f;   // d <= 32: kpad32 ||c||^2 in 32x32 accumulator order
   int2 *tlist;    // TL_SEGS x TL_CAP undecided (offset, prev) per screen wave
   int32_t *tcount; // TL_SEGS entries used per screen wave
   int32_t *queue; // n_queue sample indices for the exact re-check
@@ -63,6 +65,7 @@ constexpr int TL_SEGS = 8192;
 
 // MFMA fragment tiling of the centres: 16 centres x 16 dims per 1 KB block.
 __host__ __device__ inline int64_t kpad16(int64_t k) { return (k + 15) / 16 * 16; }
+__host__ __device__ inline int64_t kpad32(int64_t k) { return (k + 31) / 32 * 32; }
 __host__ __device__ inline int64_t dpad16(int64_t d) { return (d + 15) / 16 * 16; }
 __host__ __device__ inline int64_t dpad32(int64_t d) { return (d + 31) / 32 * 32; }
 

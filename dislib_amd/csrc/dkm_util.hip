@@ -44,6 +44,8 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
   b += round_up(kpad16(k) * dpad32(d) * 4, 256);  // cfrag
   b += round_up(kpad16(k) * 4, 256);  // cnpad
   b += round_up(kpad16(k) * dpad32(d) * 4, 256);  // bfrag (hi + lo bf16)
+  b += round_up(kpad32(k) * 32 * 4, 256);         // b32frag
+  b += round_up(kpad32(k) * 4, 256);              // cn32f
   b += (size_t)TL_SEGS * TL_CAP * 8;  // tlist
   b += (size_t)TL_SEGS * 4;           // tcount
   b += round_up(n_queue * 4, 256);    // queue
@@ -70,6 +72,10 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   p += round_up(kpad16(k) * 4, 256);
   v->bfrag = (uint16_t *)p;
   p += round_up(kpad16(k) * dpad32(d) * 4, 256);
+  v->b32frag = (uint16_t *)p;
+  p += round_up(kpad32(k) * 32 * 4, 256);
+  v->cn32f = (float *)p;
+  p += round_up(kpad32(k) * 4, 256);
   v->tlist = (int2 *)p;
   p += (size_t)TL_SEGS * TL_CAP * 8;
   v->tcount = (int32_t *)p;
@@ -158,6 +164,31 @@ __global__ void __launch_bounds__(256) k_frag(const double *__restrict__ C,
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < kp;
        c += (int64_t)gridDim.x * blockDim.x)
     v.cnpad[c] = c < k ? v.cn32[c] : 0x1.0p100f;
+  if (d > 32) return;
+  // 32x32x16 order (k_screen_w32): block cb, K-slice ks, lane l = (r, h),
+  // element j <- -2 c[cb*32 + r][16h + 8ks + j]; |c|^2 of accumulator
+  // register g of lane half h = centre cb*32 + (g & 3) + 8 (g >> 2) + 4h
+  const int64_t nb32 = kpad32(k) / 32;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       e < nb32 * 1024; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cb = e >> 10, w = e & 1023;
+    const int ks = (int)(w >> 9), l = (int)((w >> 3) & 63), j = (int)(w & 7);
+    const int64_t c = cb * 32 + (l & 31);
+    const int64_t t = 16 * (l >> 5) + 8 * ks + j;
+    const double x = (c < k && t < d) ? -2.0 * C[c * d + t] : 0.0;
+    const __bf16 hi = (__bf16)(float)x;
+    const __bf16 lo = (__bf16)(float)(x - (double)(float)hi);
+    uint16_t *dst = v.b32frag + (cb * 2 + ks) * 1024;
+    dst[l * 8 + j] = __builtin_bit_cast(uint16_t, hi);
+    dst[512 + l * 8 + j] = __builtin_bit_cast(uint16_t, lo);
+  }
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       e < nb32 * 32; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cb = e >> 5;
+    const int hh = (int)((e >> 4) & 1), g = (int)(e & 15);
+    const int64_t c = cb * 32 + (g & 3) + 8 * (g >> 2) + 4 * hh;
+    v.cn32f[e] = c < k ? v.cn32[c] : 0x1.0p100f;
+  }
 }
 
 // ---------------------------------------------------------------------------
