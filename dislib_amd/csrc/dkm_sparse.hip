@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "dkm_internal.h"
@@ -66,6 +67,79 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Centres per lane known at compile time (k <= 64 * KPL): the row's stored
+// entries are loaded once, 64 at a time (lane e holds entry e), and walked
+// in order by readlane, so each entry's C^T row loads (512 B per 64
+// centres) issue back to back instead of behind an index load per centre
+// group.  Every centre's dot still runs over the entries in stored order
+// (product, then add), exactly as above.
+template <int KPL>
+__global__ void __launch_bounds__(256)
+    k_csr_assign_r(const int64_t *__restrict__ indptr,
+                   const int32_t *__restrict__ indices,
+                   const double *__restrict__ data, int64_t n, int d,
+                   const double *__restrict__ CT, const double *__restrict__ yy,
+                   int k, int32_t *labels, double *acc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave; i < n; i += nwaves) {
+    const int64_t a = indptr[i], b = indptr[i + 1];
+    double xx = 0.0;
+    double dot[KPL];
+#pragma unroll
+    for (int g = 0; g < KPL; ++g) dot[g] = 0.0;
+    for (int64_t c0 = a; c0 < b; c0 += 64) {
+      const int cnt = (int)std::min<int64_t>(64, b - c0);
+      int myi = 0;
+      double myv = 0.0;
+      if (lane < cnt) {
+        myi = indices[c0 + lane];
+        myv = data[c0 + lane];
+      }
+      const int64_t mv = __double_as_longlong(myv);
+#pragma unroll 4
+      for (int e = 0; e < cnt; ++e) {
+        const int idx = __builtin_amdgcn_readlane(myi, e);
+        const int lo = __builtin_amdgcn_readlane((int)(mv & 0xffffffff), e);
+        const int hi = __builtin_amdgcn_readlane((int)(mv >> 32), e);
+        const double val = __longlong_as_double(
+            ((int64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+        xx = xx + val * val;
+        const double *row = CT + (int64_t)idx * k;
+#pragma unroll
+        for (int g = 0; g < KPL; ++g) {
+          const int j = lane + 64 * g;
+          if (j < k) dot[g] = dot[g] + val * row[j];
+        }
+      }
+    }
+    double best = INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int g = 0; g < KPL; ++g) {
+      const int j = lane + 64 * g;
+      if (j < k) {
+        double dd = -2.0 * dot[g];
+        dd = dd + xx;
+        dd = dd + yy[j];
+        const double dist = sqrt(dd > 0.0 ? dd : 0.0);
+        if (dist < best || bi == 0x7fffffff) {
+          best = dist;
+          bi = j;
+        }
+      }
+    }
+    wave_argmin(best, bi);
+    if (lane == 0 && labels) labels[i] = bi;
+    if (acc) {
+      for (int64_t v = a + lane; v < b; v += 64)
+        atomic_add_f64(acc + (int64_t)bi * d + indices[v], data[v]);
+      if (lane == 0) atomic_add_f64(acc + (int64_t)k * d + bi, 1.0);
+    }
+  }
+}
+
 static int csr_assign(const int64_t *indptr, const int32_t *indices,
                       const double *data, int64_t n, int64_t d,
                       const double *C, int64_t k, const void *ws, size_t wsb,
@@ -85,9 +159,23 @@ static int csr_assign(const int64_t *indptr, const int32_t *indices,
       hipGetDeviceProperties(&p, dev) == hipSuccess)
     cus = p.multiProcessorCount;
   const int64_t blocks = std::min<int64_t>((n + 3) / 4, (int64_t)cus * 16);
-  k_csr_assign<<<(unsigned)std::max<int64_t>(1, blocks), 256, 0,
-                 (hipStream_t)stream>>>(indptr, indices, data, n, (int)d,
-                                        v.ct64, v.cn64, (int)k, labels, acc);
+  const unsigned g = (unsigned)std::max<int64_t>(1, blocks);
+  hipStream_t s = (hipStream_t)stream;
+#define DKM_CSR_R(KPL)                                                       \
+  k_csr_assign_r<KPL><<<g, 256, 0, s>>>(indptr, indices, data, n, (int)d,     \
+                                        v.ct64, v.cn64, (int)k, labels, acc)
+  if (getenv("DKM_CSR_OLD") || k > 512)
+    k_csr_assign<<<g, 256, 0, s>>>(indptr, indices, data, n, (int)d, v.ct64,
+                                   v.cn64, (int)k, labels, acc);
+  else if (k <= 64)
+    DKM_CSR_R(1);
+  else if (k <= 128)
+    DKM_CSR_R(2);
+  else if (k <= 256)
+    DKM_CSR_R(4);
+  else
+    DKM_CSR_R(8);
+#undef DKM_CSR_R
   return check_launch(who);
 }
 

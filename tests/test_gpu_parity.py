@@ -219,6 +219,44 @@ def test_f07_sparse_csr():
     _close(km2.centers, g["dense_centers"], RTOL64)
 
 
+@pytest.mark.parametrize("n,d,k,per_row,seed", [
+    (2000, 400, 200, 90, 0),    # > 64 stored entries per row, 4 centres/lane
+    (3000, 5000, 256, 10, 1),   # C5 shape (scaled): 10 nnz/row, k = 256
+    (1500, 300, 60, 5, 2),      # 1 centre per lane
+    (1000, 200, 600, 20, 3)])   # k > 512: the per-centre-group kernel
+def test_csr_predict_and_partial_sum_vs_oracle(n, d, k, per_row, seed):
+    """CSR assignment (k_csr_assign_r / k_csr_assign) against the oracle's
+    sklearn-order arithmetic: labels bit-exact, sums 1e-12."""
+    from dislib_amd import _device, _lib
+    rng = np.random.default_rng(seed)
+    gap = max(1, d // per_row - 1)
+    cols = np.cumsum(rng.integers(1, gap + 1, (n, per_row)), axis=1) - 1
+    indptr = np.arange(0, n * per_row + 1, per_row)
+    xs = sp.csr_matrix((rng.random(n * per_row),
+                        cols.reshape(-1).astype(np.int32), indptr),
+                       shape=(n, d))
+    C = xs[rng.choice(n, k, replace=False)].toarray() + \
+        rng.random((k, d)) * 0.05
+    rl, rs, rc = orc.partial_sum(xs, sp.csr_matrix(C), sparse=True)
+    dev = torch.device("cuda")
+    ds = _load(xs, n)
+    dd = ds._device_data()
+    Ct = torch.from_numpy(C).to(dev)
+    ws = _device.Workspace(k, d, dd.n, dev)
+    acc = torch.empty(k * (d + 1), dtype=torch.float64, device=dev)
+    lab = torch.empty(dd.n, dtype=torch.int32, device=dev)
+    _device.prepare(Ct, ws, acc, csr=True)
+    _device.partial_sum(dd, Ct, ws, lab, acc, _lib.MODE_AUTO)
+    assert np.array_equal(lab.cpu().numpy(), rl)
+    a = acc.cpu().numpy()
+    _close(a[:k * d].reshape(k, d), np.asarray(rs.todense())
+           if sp.issparse(rs) else rs, 1e-12)
+    assert np.array_equal(a[k * d:], np.asarray(rc, dtype=np.float64))
+    lab2 = torch.full((dd.n,), -7, dtype=torch.int32, device=dev)
+    _device.predict(dd, Ct, ws, lab2, _lib.MODE_AUTO)
+    assert np.array_equal(lab2.cpu().numpy(), rl)
+
+
 # ---------------------------------------------------------------------------
 # kernel-level parity against the oracle on seeded inputs
 # ---------------------------------------------------------------------------

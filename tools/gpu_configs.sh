@@ -15,4 +15,6 @@ step() {  # name limit cmd...
 step c3 300 python bench.py --n 125000000 --d 64 --k 1000 --steps 3 --warmup 1 --no-cpu
 step c3exact 300 python bench.py --n 10000000 --d 64 --k 1000 --steps 1 --warmup 0 --no-cpu --mode exact
 step c3prof 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/${TAG}_c3prof -o run -- python bench.py --n 125000000 --d 64 --k 1000 --steps 2 --warmup 1 --no-cpu
+step c5 400 python tools/bench_csr.py --n 10000000 --d 10000 --nnz 10 --k 256 --steps 5
+step c4exact 400 python bench.py --n 200000 --d 1024 --k 4096 --steps 1 --warmup 0 --no-cpu
 echo "== done"
