@@ -46,7 +46,7 @@ class DeviceData:
         self.d = int(dataset.n_features)
         self.sparse = bool(dataset.sparse)
         if self.sparse:
-            self._upload_csr(subsets)
+            self._upload_csr(subsets, getattr(dataset, "_host_image", None))
         else:
             self._upload_dense(subsets)
 
@@ -82,12 +82,15 @@ class DeviceData:
         self.int_input = any(np.issubdtype(a.dtype, np.integer) for a in arrs)
 
     # -- CSR ---------------------------------------------------------------
-    def _upload_csr(self, subsets):
+    def _upload_csr(self, subsets, image=None):
         import scipy.sparse as sp
         t = torch()
-        mats = [sp.csr_matrix(s.samples) for s in subsets]
-        m = sp.vstack(mats, format="csr") if mats else \
-            sp.csr_matrix((0, self.d))
+        if image is not None and image.shape == (self.n, self.d):
+            m = image      # file loaders: the parser's concatenated output
+        else:
+            mats = [sp.csr_matrix(s.samples) for s in subsets]
+            m = sp.vstack(mats, format="csr") if mats else \
+                sp.csr_matrix((0, self.d))
         # keep each row's stored order: it is the reference's dot order
         self.dtype = np.float64
         self.indptr = t.from_numpy(m.indptr.astype(np.int64)).to(self.device)

@@ -51,6 +51,11 @@ SIGNATURES = {
     "dkm_make_blobs_f64": (_i32, [_p, _i64, _i64, _i64, _i64, _u64, _f64,
                                   _f64, _p, _p]),
     "dkm_screen_stats": (_i32, [_p, ctypes.POINTER(_i64), _p]),
+    # host-side loaders (no GPU)
+    "dkm_libsvm_count": (_i32, [_p, _i64, _i32, _p]),
+    "dkm_libsvm_parse": (_i32, [_p, _i64, _i32, _p, _p, _p, _p, _p]),
+    "dkm_txt_count": (_i32, [_p, _i64, _i32, _i32, _p]),
+    "dkm_txt_parse": (_i32, [_p, _i64, _i32, _i64, _i32, _p, _p]),
 }
 
 _LIB = None

@@ -129,6 +129,7 @@ class Dataset(object):
         self._labels = None
         self._sparse = sparse
         self._device = None        # DeviceData cache
+        self._host_image = None    # loader's concatenated CSR (one upload)
 
     def __getitem__(self, item):
         return self._subsets.__getitem__(item)
@@ -205,6 +206,7 @@ class Dataset(object):
         self._samples = None
         self._labels = None
         self._device = None
+        self._host_image = None
 
     def _compute_min_max(self):
         mm = []

@@ -35,6 +35,7 @@ extern "C" {
 #define DKM_E_ARG 10001       /* invalid argument / shape                    */
 #define DKM_E_WORKSPACE 10002 /* workspace too small                         */
 #define DKM_E_LAUNCH 10003    /* kernel launch failed                        */
+#define DKM_E_PARSE 10004     /* malformed input text (loaders)              */
 
 /* assignment modes (flags) */
 #define DKM_MODE_AUTO 0     /* library picks: SCREEN32 when profitable       */
@@ -154,6 +155,39 @@ int dkm_make_blobs_f64(double *X, int64_t row0, int64_t n, int64_t d,
 /* Diagnostics of the last SCREEN32 call on this workspace (device -> host,
  * synchronous on `stream`): number of samples sent to the exact re-check.  */
 int dkm_screen_stats(const void *ws, int64_t *n_rechecked, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Dataset loaders.  HOST functions: `buf`
+ * and every output are host pointers; no GPU is touched.  `buf` holds
+ * the whole file (len bytes); lines end at "\n", "\r\n" or "\r" (Python
+ * text mode).  nthreads <= 0 = all hardware threads.  Call *_count first
+ * to size the outputs.  `row_line[r]` = 0-based raw line of row r, so the
+ * caller can cut Subsets every `subset_size` raw lines exactly like
+ * `_load_file` (dislib/data/base.py:145-164).
+ * --------------------------------------------------------------------- */
+
+/* counts[4] <- {raw lines, rows, stored entries, threads used}.
+ * Replaces the tokenizer of sklearn's load_svmlight_file as called by
+ * `_read_libsvm` / `_read_file` (dislib/data/base.py:200-238). */
+int dkm_libsvm_count(const char *buf, int64_t len, int nthreads,
+                     int64_t *counts);
+/* indptr[rows+1], indices[nnz] (as written: the caller applies sklearn's
+ * zero_based="auto" shift per chunk), data[nnz], y[rows] (targets),
+ * row_line[rows].  DKM_E_PARSE with sklearn's message for a bad number,
+ * a negative index or indices that are not strictly increasing. */
+int dkm_libsvm_parse(const char *buf, int64_t len, int nthreads,
+                     int64_t *indptr, int32_t *indices, double *data,
+                     double *y, int64_t *row_line);
+/* counts[4] <- {raw lines, rows, fields of the first row, threads used}.
+ * delimiter: a byte, or 0 for whitespace runs (numpy's delimiter=None).
+ * Replaces np.genfromtxt in `_read_lines` / `_read_file`
+ * (dislib/data/base.py:188, :212). */
+int dkm_txt_count(const char *buf, int64_t len, int delimiter, int nthreads,
+                  int64_t *counts);
+/* out[rows x n_cols] row-major fp64 (unconvertible/empty field = NaN),
+ * row_line[rows].  DKM_E_PARSE if a row has another number of fields. */
+int dkm_txt_parse(const char *buf, int64_t len, int delimiter, int64_t n_cols,
+                  int nthreads, double *out, int64_t *row_line);
 
 #ifdef __cplusplus
 }
