@@ -71,6 +71,15 @@ def load_txt_files(path, n_features, delimiter=",", label_col=None):
 
 
 # ---------------------------------------------------------------------------
+def _threads():
+    """Parser threads: OMP_NUM_THREADS if set, else the CPUs this process
+    may run on (capped at 32)."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    return max(1, min(len(os.sched_getaffinity(0)), 32))
+
+
 def _read(path):
     with open(path, "rb") as f:
         return f.read()
@@ -89,10 +98,11 @@ def _raise(rc, what):
     raise _lib.DkmError("%s failed (code %d): %s" % (what, rc, msg))
 
 
-def parse_libsvm(buf, nthreads=0):
+def parse_libsvm(buf, nthreads=None):
     """Tokenise a whole LibSVM byte buffer: returns (n_lines, indptr int64,
     indices int32 (unshifted), data fp64, y fp64, row_line int64)."""
     so = _lib.load()
+    nthreads = _threads() if nthreads is None else int(nthreads)
     b = np.frombuffer(buf, np.uint8)
     counts = np.zeros(4, np.int64)
     _raise(so.dkm_libsvm_count(_addr(b), b.size, nthreads, _addr(counts)),
@@ -109,7 +119,7 @@ def parse_libsvm(buf, nthreads=0):
     return n_lines, indptr, indices, data, y, row_line
 
 
-def parse_txt(buf, delimiter=",", nthreads=0):
+def parse_txt(buf, delimiter=",", nthreads=None):
     """Tokenise a whole delimited text buffer: returns (n_lines, values
     (rows x cols fp64, NaN where a field does not convert), row_line)."""
     if delimiter is None:
@@ -122,6 +132,7 @@ def parse_txt(buf, delimiter=",", nthreads=0):
                              "whitespace), got %r" % (delimiter,))
         dl = db[0]
     so = _lib.load()
+    nthreads = _threads() if nthreads is None else int(nthreads)
     b = np.frombuffer(buf, np.uint8)
     counts = np.zeros(4, np.int64)
     _raise(so.dkm_txt_count(_addr(b), b.size, dl, nthreads, _addr(counts)),

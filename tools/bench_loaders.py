@@ -64,7 +64,9 @@ def main():
                     help="rows of the file the (slow) reference path reads")
     a = ap.parse_args()
     tmp = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
-    out = {"cores": len(os.sched_getaffinity(0))}
+    from dislib_amd.data.base import _threads
+    out = {"parser_threads": _threads(),
+           "affinity_cpus": len(os.sched_getaffinity(0))}
     p = os.path.join(tmp, "x.svm")
     write_libsvm(p, a.rows, a.d, a.nnz)
     mb = os.path.getsize(p) / 1e6
