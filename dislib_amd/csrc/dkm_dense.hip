@@ -588,7 +588,10 @@ __device__ __forceinline__ bool resolve_lane(
   };
   float b1 = INFINITY, b2 = INFINITY;
   int i1 = 0;
-#pragma unroll 2
+#ifndef DKM_S1_UNROLL
+#define DKM_S1_UNROLL 4
+#endif
+#pragma unroll DKM_S1_UNROLL
   for (int jc = 0; jc < k; ++jc) {
     const float sc = score(jc);
     i1 = sc < b1 ? jc : i1;
@@ -1043,8 +1046,12 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
 // argument and the same list / label / accumulation contract as k_screen.
 // ---------------------------------------------------------------------------
 constexpr int SBW = 256;  // k_screen_w32 block: 4 waves, 3 blocks per CU
+#ifndef DKM_W32_WPE
+#define DKM_W32_WPE 3
+#endif
 template <class TX>
-__global__ void __launch_bounds__(SBW) __attribute__((amdgpu_waves_per_eu(3)))
+__global__ void __launch_bounds__(SBW) __attribute__((
+    amdgpu_waves_per_eu(DKM_W32_WPE)))
     k_screen_w32(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
                  int k, WsView v, int32_t *__restrict__ lab_out, double *acc,
                  int amode, int64_t base, int use_list) {
@@ -1421,6 +1428,9 @@ __global__ void __launch_bounds__(BLOCK)
   if (amode & AM_INLDS) flush_lds_acc(lds_acc, acc, k, d);
 }
 
+#ifndef DKM_LIST_SPREAD
+#define DKM_LIST_SPREAD 1
+#endif
 // The screen's per-wave lists (WsView::tlist/tcount, nseg segments): lane
 // per listed sample (resolve_lane), fp32 centres in LDS.  No label scan:
 // the work is proportional to the undecided samples only.
@@ -1454,11 +1464,25 @@ __global__ void __launch_bounds__(BLOCK)
                                 v.cn32, dp,
                                 cm, v.ct64, lab_out, amode, at);
   };
+#if DKM_LIST_SPREAD
+  // (segment, 64-sample batch) pairs dealt round-robin over all waves, batch
+  // index major: every resident wave gets work and the segments' row loads
+  // overlap across waves.  Wave-uniform loop; empty batches are skipped.
+  for (int64_t L = wv; L < (int64_t)nseg * (TL_CAP / 64); L += nwv) {
+    const int64_t sg = L % nseg;
+    const int t0 = (int)(L / nseg) * 64;
+    const int cnt = v.tcount[sg];
+    if (t0 == 0) mine += cnt;
+    if (t0 >= cnt) continue;
+    const int2 *e = v.tlist + sg * TL_CAP;
+    {
+#else
   for (int64_t sg = wv; sg < nseg; sg += nwv) {
     const int cnt = v.tcount[sg];
     mine += cnt;
     const int2 *e = v.tlist + sg * TL_CAP;
     for (int t0 = 0; t0 < cnt; t0 += 64) {
+#endif
       int2 it = make_int2(0, 0);
       bool ok = true;
       if (t0 + lane < cnt) {
@@ -1747,9 +1771,10 @@ static int launch_list_t(const TX *X, int d, int64_t ldx, int k,
                          hipStream_t s) {
   const void *kf = (const void *)k_recheck_list<MAXD, VEC, TX>;
   const int per_cu = resident_blocks(kf, BLOCK, lds);
+  const int64_t units = DKM_LIST_SPREAD ? (int64_t)nseg * (TL_CAP / 64) : nseg;
   const int64_t g = std::max<int64_t>(
       1, std::min<int64_t>((int64_t)dev_info().cus * per_cu,
-                           (nseg + BLOCK / 64 - 1) / (BLOCK / 64)));
+                           (units + BLOCK / 64 - 1) / (BLOCK / 64)));
   k_recheck_list<MAXD, VEC, TX><<<(unsigned)g, BLOCK, lds, s>>>(
       X, d, ldx, k, v, lab_out, acc, amode, base, nseg);
   return check_launch("list re-check");
@@ -1918,7 +1943,11 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   // and k_label_sums accumulates from them (delta: against a copy of the
   // previous labels in the label scratch)
   const bool lds_fits = fb + a_bytes <= LDS_BUDGET;
-  const bool post = acc_kind != 0 && !lds_fits && !getenv("DKM_NO_POST") &&
+  // DKM_DELTA_POST: delta sums from k_label_sums even when they fit LDS
+  // (the screen then needs only the fragments' LDS: more blocks per CU)
+  const bool force_post = acc_kind == 2 && getenv("DKM_DELTA_POST");
+  const bool post = acc_kind != 0 && (!lds_fits || force_post) &&
+                    !getenv("DKM_NO_POST") &&
                     (acc_kind == 1 || (labels && nq >= n));
   const int32_t *prevbuf = nullptr;
   if (post && acc_kind == 2) {

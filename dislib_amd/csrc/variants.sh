@@ -10,7 +10,8 @@ while [ $# -ge 2 ]; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off \
       -fno-slp-vectorize $defs -c $f.hip -o $d/$f.o &
   done
+  g++ -O3 -std=c++17 -fPIC -pthread -c dkm_io.cpp -o $d/dkm_io.o &
   wait
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../libdkm_$name.so $d/*.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -pthread -o ../libdkm_$name.so $d/*.o
   echo built ../libdkm_$name.so
 done
