@@ -1046,6 +1046,10 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
 // argument and the same list / label / accumulation contract as k_screen.
 // ---------------------------------------------------------------------------
 constexpr int SBW = 256;  // k_screen_w32 block: 4 waves, 3 blocks per CU
+// cache policy of k_screen_w32's streaming row loads (0 = default; 2 = NT)
+#ifndef DKM_XLOAD_AUX
+#define DKM_XLOAD_AUX 0
+#endif
 #ifndef DKM_W32_WPE
 #define DKM_W32_WPE 3
 #endif
@@ -1113,7 +1117,7 @@ __global__ void __launch_bounds__(SBW) __attribute__((
           for (int p4 = 0; p4 < 4; ++p4) {
             const double2 v2 = __builtin_bit_cast(
                 double2, __builtin_amdgcn_raw_buffer_load_b128(
-                             rx, lane_off, o + 16 * p4, 0));
+                             rx, lane_off, o + 16 * p4, DKM_XLOAD_AUX));
             tile[8 * ks + 2 * p4] = v2.x;
             tile[8 * ks + 2 * p4 + 1] = v2.y;
           }
@@ -1122,7 +1126,7 @@ __global__ void __launch_bounds__(SBW) __attribute__((
           for (int p4 = 0; p4 < 2; ++p4) {
             const float4 v4 = __builtin_bit_cast(
                 float4, __builtin_amdgcn_raw_buffer_load_b128(
-                            rx, lane_off, o + 16 * p4, 0));
+                            rx, lane_off, o + 16 * p4, DKM_XLOAD_AUX));
             tile[8 * ks + 4 * p4] = v4.x;
             tile[8 * ks + 4 * p4 + 1] = v4.y;
             tile[8 * ks + 4 * p4 + 2] = v4.z;
