@@ -285,3 +285,25 @@ def test_libsvm_loader_feeds_kmeans_host_image(tmp_path):
     assert _same(img.data, st.data)
     ds.append(ds[0])
     assert ds._host_image is None      # invalidated by a mutation
+
+
+def test_parser_abi_argument_checks():
+    """C-ABI error behaviour of the loader entry points (host-only)."""
+    import ctypes
+    from dislib_amd import _lib
+    so = _lib.load()
+    cnt = np.zeros(4, np.int64)
+    p = ctypes.c_void_p(cnt.ctypes.data)
+    assert so.dkm_libsvm_count(None, 5, 1, p) == 10001        # NULL buffer
+    assert b"bad arguments" in so.dkm_last_error()
+    assert so.dkm_txt_count(None, 0, 300, 1, p) == 10001      # bad delimiter
+    assert so.dkm_libsvm_count(None, 0, 1, p) == 0            # empty input
+    assert list(cnt[:3]) == [0, 0, 0]
+    buf = np.frombuffer(b"1 1:2 1:3\n", np.uint8)
+    ptr = np.zeros(2, np.int64)
+    ind, dat = np.empty(2, np.int32), np.empty(2)
+    y, rl = np.empty(1), np.empty(1, np.int64)
+    a = [ctypes.c_void_p(x.ctypes.data) for x in (buf, ptr, ind, dat, y, rl)]
+    rc = so.dkm_libsvm_parse(a[0], buf.size, 1, a[1], a[2], a[3], a[4], a[5])
+    assert rc == 10004 and b"sorted and unique" in so.dkm_last_error()
+    assert b"(line 1)" in so.dkm_last_error()
