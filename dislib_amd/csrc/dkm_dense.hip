@@ -1999,6 +1999,45 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   return 0;
 }
 
+// d > 128: the bf16x3 GEMM screen (dkm_gemm.hip), which also resolves the
+// samples it leaves open with the reference arithmetic.  Sums come from k_label_sums (X is read once more,
+// lanes over features) unless the previous labels cannot be kept for a
+// delta pass (label scratch smaller than n): then the merge step adds the
+// changed rows itself with fp64 atomics.
+template <class TX>
+static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
+                       const double *C, int k, const WsView &v, size_t wsb,
+                       int32_t *labels, double *acc, int acc_kind,
+                       hipStream_t s) {
+  const size_t fixed = (size_t)((const char *)v.queue - (const char *)v.hdr);
+  const int64_t nq =
+      std::min<int64_t>((int64_t)((wsb - fixed) / 4), INT32_MAX);
+  if (!labels && nq < 1)
+    return fail(DKM_E_WORKSPACE, "gemm: no label scratch");
+  const int64_t chunk = labels ? n : nq;
+  const bool post =
+      acc_kind != 0 && (acc_kind == 1 || (labels && nq >= n));
+  const int32_t *prevbuf = nullptr;
+  if (post && acc_kind == 2) {
+    if (hipMemcpyAsync(v.queue, labels, (size_t)n * 4,
+                       hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return fail(DKM_E_LAUNCH, "gemm: label copy");
+    prevbuf = v.queue;
+  }
+  const int skind = post ? 0 : acc_kind;
+  for (int64_t base = 0; base < n; base += chunk) {
+    const int64_t end = std::min(n, base + chunk);
+    int32_t *lab_out = labels ? labels : v.queue - base;
+    int r = gemm_screen<TX>(X, base, end, d, ldx, C, k, v, lab_out,
+                            skind ? acc : nullptr, skind == 2, s);
+    if (r) return r;
+    if (post && (r = launch_label_sums<TX>(X, base, end, d, ldx, lab_out,
+                                           prevbuf, k, acc, s)))
+      return r;
+  }
+  return 0;
+}
+
 template <class TX>
 static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                   const double *C, int64_t k, const void *ws, size_t wsb,
@@ -2014,10 +2053,17 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
     return fail(DKM_E_ARG, std::string(who) + ": nothing to write");
   hipStream_t s = (hipStream_t)stream;
   if (mode == DKM_MODE_AUTO)
-    mode = screen_ok(k, d) ? DKM_MODE_SCREEN_BF16X3 : DKM_MODE_EXACT;
+    mode = screen_ok(k, d) || gemm_path(k, d) ? DKM_MODE_SCREEN_BF16X3
+                                              : DKM_MODE_EXACT;
   if (mode == DKM_MODE_EXACT)
     return launch_exact<TX>(X, n, (int)d, ldx, C, (int)k, labels, acc,
                             acc_kind, s);
+  if (mode == DKM_MODE_SCREEN_BF16X3 && gemm_path(k, d)) {
+    WsView v;
+    if (int r = ws_view(ws, wsb, k, d, &v)) return r;
+    return launch_gemm<TX>(X, n, (int)d, ldx, C, (int)k, v, wsb, labels, acc,
+                           acc_kind, s);
+  }
   if (mode == DKM_MODE_SCREEN32 || mode == DKM_MODE_SCREEN_BF16X3) {
     if (!screen_ok(k, d))
       return launch_exact<TX>(X, n, (int)d, ldx, C, (int)k, labels, acc,

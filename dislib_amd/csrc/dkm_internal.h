@@ -32,13 +32,39 @@ struct WsHeader {
   uint32_t qcount;          // samples queued for exact re-check this call
   uint32_t pad0;
   uint64_t rechecked_total; // diagnostics
-  uint64_t reserved[8];
+  uint32_t gcount;          // GEMM screen: candidate-list entries (per chunk)
+  uint32_t gcount2;         // GEMM screen: full-scan entries (per chunk)
+  uint64_t reserved[7];
 };
-constexpr uint64_t WS_MAGIC = 0x444b4d5753303031ull;  // "DKMWS001"
+constexpr uint64_t WS_MAGIC = 0x444b4d5753303032ull;  // "DKMWS002"
 constexpr size_t WS_HDR = 256;
 
 __host__ __device__ inline int64_t round_up(int64_t a, int64_t b) {
   return (a + b - 1) / b * b;
+}
+
+// ---------------------------------------------------------------------------
+// Large-d GEMM screen (dkm_gemm.hip, d > 128): tiles of GT rows x GBK
+// features, bf16 hi/lo split, 128-B rows with XOR-swizzled 16-B chunks.
+// ---------------------------------------------------------------------------
+constexpr int GT = 256;                 // rows per tile (centres or samples)
+constexpr int GBK = 32;                 // features per K-stage
+constexpr int GSTAGE = GT * GBK * 4;    // bytes per operand tile per stage
+constexpr int GTOP = 4;                 // (score, centre) pairs kept per sample
+
+__host__ __device__ inline int64_t kpad256(int64_t k) { return (k + 255) / 256 * 256; }
+
+// GEMM screen eligibility: the register-tile screen takes d <= 128
+inline bool gemm_path(int64_t k, int64_t d) {
+  return d > 128 && k >= 2 && k <= 32767;
+}
+// samples per split chunk: <= 256 MB of split rows, a multiple of GT
+inline int64_t gemm_chunk(int64_t d) {
+  const int64_t per = ((d + 31) / 32 * 32) * 4;
+  int64_t m = ((int64_t)1 << 28) / per / GT * GT;
+  if (m > 65536) m = 65536;
+  if (m < GT) m = GT;
+  return m;
 }
 
 struct WsView {
@@ -54,6 +80,13 @@ struct WsView {
   float *cn32f;   // d <= 32: kpad32 ||c||^2 in 32x32 accumulator order
   int2 *tlist;    // TL_SEGS x TL_CAP undecided (offset, prev) per screen wave
   int32_t *tcount; // TL_SEGS entries used per screen wave
+  // GEMM screen (gemm_path only; else NULL)
+  char *gfrag;     // kpad256 x dpad32 centre tiles (-2c, bf16 hi/lo)
+  float *gcn;      // kpad256 fp32 ||c||^2, 2^100 for padding centres
+  char *gxs;       // gemm_chunk samples: split tiles of the current chunk
+  float *gxn;      // gemm_chunk fp32 upper bounds of ||x||
+  int2 *gpart;     // gemm_chunk x kpad256/GT x GTOP (score bits, centre)
+  int64_t gchunk;  // samples per split chunk
   int32_t *queue; // n_queue sample indices for the exact re-check
 };
 
@@ -104,12 +137,16 @@ __device__ __forceinline__ double pw_leaf(const F &f, int64_t lo, int64_t n) {
 }
 
 // Recursive halving above 128 elements, as an explicit post-order walk.
-template <class F>
-__device__ double pw_block(const F &f, int64_t lo, int64_t n) {
-  if (n <= 128) return pw_leaf(f, lo, n);
-  int64_t flo[16], fn[16];
-  double fleft[16];
-  int fstate[16];
+// n <= 8192 (one iterator buffer): at most 6 halvings, so 8 stack levels.
+// `leaf(lo, n)` returns the value of a leaf block (n <= 128); leaves are
+// visited left to right.
+template <class LEAF>
+__device__ double pw_tree(LEAF &&leaf, int64_t lo, int64_t n) {
+  if (n <= 128) return leaf(lo, n);
+  int64_t flo[8];
+  int fn[8];
+  double fleft[8];
+  int fstate[8];
   int sp = 0;
   flo[0] = lo;
   fn[0] = n;
@@ -118,7 +155,7 @@ __device__ double pw_block(const F &f, int64_t lo, int64_t n) {
   for (;;) {
     if (!have) {
       if (fn[sp] <= 128) {
-        val = pw_leaf(f, flo[sp], fn[sp]);
+        val = leaf(flo[sp], (int64_t)fn[sp]);
         have = true;
       } else {
         int64_t n2 = fn[sp] / 2;
@@ -145,6 +182,13 @@ __device__ double pw_block(const F &f, int64_t lo, int64_t n) {
       val = fleft[sp] + val;
     }
   }
+}
+
+template <class F>
+__device__ double pw_block(const F &f, int64_t lo, int64_t n) {
+  return pw_tree(
+      [&](int64_t a, int64_t m) -> double { return pw_leaf(f, a, m); }, lo,
+      n);
 }
 
 template <class F>
@@ -240,5 +284,19 @@ __device__ __forceinline__ void wave_argmin(double &dist, int &idx) {
 __device__ __forceinline__ void atomic_add_f64(double *p, double v) {
   unsafeAtomicAdd(p, v);  // global_atomic_add_f64 (no CAS loop on gfx950)
 }
+
+// ---------------------------------------------------------------------------
+// dkm_gemm.hip entry points (host side)
+// ---------------------------------------------------------------------------
+// centre tiles + padded norms for the GEMM screen (after k_prepare)
+int gemm_prepare(const double *C, int64_t k, int64_t d, const WsView &v,
+                 hipStream_t s);
+// Screen samples [base, end): labels (or -(prev + 2) for the exact re-check,
+// counted in hdr->qcount).  acc != NULL: the merge step also moves rows
+// between the sums with fp64 atomics (delta = true: only changed labels).
+template <class TX>
+int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
+                const double *C, int k, const WsView &v, int32_t *lab_out,
+                double *acc, bool delta, hipStream_t s);
 
 }  // namespace dkm

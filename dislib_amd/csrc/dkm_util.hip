@@ -33,6 +33,19 @@ int64_t default_queue(int64_t k, int64_t d) {
   return int64_t(1) << 22;  // 4M re-check slots (16 MB); overflow -> inline
 }
 
+// GEMM screen regions (gemm_path only)
+static size_t gemm_bytes(int64_t k, int64_t d) {
+  if (!gemm_path(k, d)) return 0;
+  const int64_t kp = kpad256(k), dp = dpad32(d), m = gemm_chunk(d);
+  size_t b = 0;
+  b += round_up(kp * dp * 4, 256);              // gfrag
+  b += round_up(kp * 4, 256);                   // gcn
+  b += round_up(m * dp * 4, 256);               // gxs
+  b += round_up(m * 4, 256);                    // gxn
+  b += round_up(m * (kp / GT) * GTOP * 8, 256); // gpart
+  return b;
+}
+
 size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
   if (n_queue <= 0) n_queue = default_queue(k, d);
   const int64_t dpad = round_up(d, 4);
@@ -48,6 +61,7 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
   b += round_up(kpad32(k) * 4, 256);              // cn32f
   b += (size_t)TL_SEGS * TL_CAP * 8;  // tlist
   b += (size_t)TL_SEGS * 4;           // tcount
+  b += gemm_bytes(k, d);
   b += round_up(n_queue * 4, 256);    // queue
   return b;
 }
@@ -80,6 +94,26 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   p += (size_t)TL_SEGS * TL_CAP * 8;
   v->tcount = (int32_t *)p;
   p += (size_t)TL_SEGS * 4;
+  v->gfrag = nullptr;
+  v->gcn = nullptr;
+  v->gxs = nullptr;
+  v->gxn = nullptr;
+  v->gpart = nullptr;
+  v->gchunk = 0;
+  if (gemm_path(k, d)) {
+    const int64_t kp = kpad256(k), dp = dpad32(d), m = gemm_chunk(d);
+    v->gchunk = m;
+    v->gfrag = p;
+    p += round_up(kp * dp * 4, 256);
+    v->gcn = (float *)p;
+    p += round_up(kp * 4, 256);
+    v->gxs = p;
+    p += round_up(m * dp * 4, 256);
+    v->gxn = (float *)p;
+    p += round_up(m * 4, 256);
+    v->gpart = (int2 *)p;
+    p += round_up(m * (kp / GT) * GTOP * 8, 256);
+  }
   v->queue = (int32_t *)p;
   const size_t fixed = (size_t)(p - (char *)ws);
   if (bytes < fixed + 256)
@@ -333,6 +367,8 @@ int dkm_prepare_centers(const double *C, int64_t k, int64_t d, int flags,
     k_frag<<<(unsigned)g, 256, 0, s>>>(C, k, d, v);
   }
   if (int r = check_launch("dkm_prepare_centers")) return r;
+  if (gemm_path(k, d))
+    if (int r = gemm_prepare(C, k, d, v, s)) return r;
   if (acc) {
     hipError_t e = hipMemsetAsync(acc, 0, (size_t)(k * (d + 1)) * 8, s);
     if (e != hipSuccess)

@@ -555,3 +555,22 @@ def test_recheck_scan_misaligned_labels(offset, kind):
         assert np.array_equal(a[6 * d:], rc.astype(np.float64))
         _close(a[:6 * d].reshape(6, d), rs, 1e-12)
     assert _device.rechecked(ws) > n // 2
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_f16_c1_full_size(mode):
+    """BASELINE configs[0] at full size, reference golden vectors
+    (tests/golden/gen_golden_big.py): make_blobs(100k x 50, 10 centres),
+    subset 10k, KMeans(10, max_iter=10, tol=1e-4, arity=50, random_state=0)
+    .fit_predict -- labels bit-exact, centres within 1e-9, same n_iter."""
+    g = load_golden("f16_c1full")
+    x, _ = make_blobs(n_samples=100_000, n_features=50, centers=10,
+                      random_state=0)
+    assert hashlib.sha256(x.tobytes()).hexdigest() == str(g["x_sha"])
+    ds = _load(x, 10_000)
+    km = _km(n_clusters=10, max_iter=10, tol=1e-4, arity=50, random_state=0,
+             mode=mode)
+    km.fit_predict(ds)
+    assert km.n_iter == int(g["n_iter"])
+    assert np.array_equal(ds.labels_int32(), g["labels"].astype(np.int32))
+    _close(km.centers, g["centers"], RTOL64)

@@ -179,3 +179,37 @@ def test_synthetic_blobs_generator_is_row_addressable():
     b, lb = orc.make_blobs_rows(40, 20, 5, 7, seed=3)
     assert np.array_equal(a[40:60], b) and np.array_equal(la[40:60], lb)
     assert np.isfinite(a).all() and 0 <= la.min() and la.max() < 7
+
+
+def test_f16_c1_full_size_bit_exact():
+    """BASELINE configs[0] at full size (100k x 50, k = 10, subset 10k,
+    tol 1e-4): the oracle reproduces the reference's fit_predict bit for
+    bit (tests/golden/gen_golden_big.py)."""
+    g = load_golden("f16_c1full")
+    x, _ = make_blobs(n_samples=100_000, n_features=50, centers=10,
+                      random_state=0)
+    assert _sha(x) == str(g["x_sha"])
+    m, lab = _fit(x, 10_000, n_clusters=10, max_iter=10, tol=1e-4, arity=50,
+                  random_state=0)
+    assert m.n_iter == int(g["n_iter"])
+    assert np.array_equal(m.centers, g["centers"])
+    assert np.array_equal(lab, g["labels"].astype(np.int64))
+    assert np.array_equal(np.array(m.trace), g["trace"])
+
+
+def test_f15_c4_fixture_is_consistent():
+    """The C4-shape fixture (reference fit at d = 1024, k = 4096; the oracle
+    at that shape takes minutes, so the GPU test compares against it
+    directly): labels, counts and the kept centre rows agree with each
+    other and with the regenerated input."""
+    g = load_golden("f15_c4mini")
+    x, _ = make_blobs(n_samples=20_000, n_features=1024, centers=4096,
+                      center_box=(-10, 10), random_state=15)
+    assert _sha(x) == str(g["x_sha"])
+    lab = g["labels"].astype(np.int64)
+    assert np.array_equal(np.bincount(lab, minlength=4096), g["counts"])
+    # the most populated cluster's centre: the mean of the samples labelled
+    # in the last assignment is NOT it (fit_predict labels precede the last
+    # update), so only check shapes and finiteness here
+    assert g["top_rows"].shape == (16, 1024)
+    assert np.isfinite(g["proj"]).all() and g["proj"].shape == (4096, 8)
