@@ -1,20 +1,25 @@
 """Lloyd-iteration throughput of dislib_amd's KMeans on MI355X.
 
-Workload (BASELINE.json configs[1]): KMeans k=100 on 100M x 32 fp64 dense
-make_blobs data per GPU, synthetic, generated on the device by the library's
-counter-based generator (100 blobs, centres U(-10,10), std 1), Subsets of 1M
-rows, initial centres np.random.seed(0); np.random.random((k, d)).
+Headline workload (BASELINE.json configs[1], the metric's config): KMeans
+k=100 on 100M x 32 fp64 dense make_blobs data per GPU, synthetic, generated
+on the device by the library's counter-based generator (k blobs, centres
+U(-10,10), std 1), Subsets of 1M rows, initial centres
+np.random.seed(0); np.random.random((k, d)).
 
 A "step" is one Lloyd iteration over all resident samples: centre prep ->
-fused assign + per-cluster sum/count (HIP) -> RCCL all-reduce of
-[sums | counts] (N > 1) -> centre update + convergence criterion (HIP) ->
-4-byte flag read.  Weak scaling: every rank owns n samples.
+fused assign + per-cluster sum/count (HIP) -> all-reduce of [sums | counts]
+(RCCL through libdkm, N > 1) -> centre update + convergence criterion
+(HIP) -> 4-byte flag read.  Weak scaling: every rank owns n samples.
 
-Prints ONE JSON line (rank 0) with metric/value/unit, the roofline of the
-dominant kernel (dkm_partial_sum, timed with HIP events on its stream) and a
-CPU baseline (the oracle, rank 0, N=1 only, bounded sample).
+Prints ONE JSON line (rank 0): metric/value/unit for the headline config,
+its roofline (the assignment call -- the dominant kernels -- timed with HIP
+events on its stream), a CPU baseline (the oracle on this host, rank 0,
+N=1 only, bounded sample), the fit_predict variant (labels written), and
+under "extra_configs" the other single-GPU BASELINE configs measured the
+same way in the same run: configs[2]'s per-GPU shard (125M x 64, k=1000,
+the north-star target) and configs[3] (10M x 1024, k=4096, fp64; MFMA).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--only-headline]
   torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -30,7 +35,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "KMeans samples·iters/sec at 1/2/4/8 GPUs + % of HBM/MFMA roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
-FP32_PEAK_TFLOPS = 157.3       # vector/matrix fp32 (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6        # fp64 vector = matrix
 
 
 def parse():
@@ -39,39 +45,57 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--n", type=int, default=100_000_000,
-                   help="samples per GPU")
+                   help="samples per GPU (headline config)")
     p.add_argument("--d", type=int, default=32)
     p.add_argument("--k", type=int, default=100)
     p.add_argument("--subset", type=int, default=1_000_000)
     p.add_argument("--mode", default="auto")
     p.add_argument("--labels", action="store_true",
-                   help="fit_predict (write labels) instead of fit")
+                   help="headline = fit_predict (labels written)")
+    p.add_argument("--only-headline", action="store_true",
+                   help="skip the fit_predict and extra-config runs")
     p.add_argument("--no-cpu", action="store_true",
-                   help="skip the CPU baseline")
+                   help="skip the CPU baselines")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--traffic-json", default=os.path.join(
         ROOT, "profiles", "r01_traffic.json"))
     return p.parse_args()
 
 
-def cpu_baseline(d, k, target_s, centers):
-    """Oracle (numpy restatement of the reference, vectorised) on the host:
-    one Lloyd iteration's partial sums, one task per Subset over a process
-    pool, BLAS threads = 1.  Bounded sample sized for ~target_s seconds."""
-    os.environ.setdefault("OMP_NUM_THREADS", "1")
-    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+# ---------------------------------------------------------------------------
+# CPU baseline: the oracle (numpy restatement of the reference, pinned to the
+# reference's golden vectors) timed on this host
+# ---------------------------------------------------------------------------
+def cpu_share():
+    """Worker processes for the CPU baseline: the CPU share the GPU box
+    grants this job (OMP_NUM_THREADS, 16 per GPU there) within the
+    affinity mask; the whole machine's thread count is reported beside."""
+    aff = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(env) if env.isdigit() and int(env) > 0 else aff
+    return max(1, min(share, aff)), aff
+
+
+def cpu_baseline(d, k, target_s, centers, n_blobs):
+    """One Lloyd iteration's partial sums on a bounded sample of the same
+    workload, one Subset per task over a process pool (BLAS threads 1),
+    then the arity-50 merge and the centre update -- the reference's task
+    graph (base.py:113-147) run by the vectorised oracle."""
+    os.environ["OMP_NUM_THREADS"] = "1"
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
     import multiprocessing as mp
     from oracle import kmeans_oracle as orc
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
-    # probe: single-core rate on a small block
-    probe = 4000
-    xb, _ = orc.make_blobs_rows(0, probe, d, k, seed=0)
+    cores, machine = cpu_share()
+    # probe: single-core rate on a small block (smaller for large k*d)
+    probe = int(max(16, min(4000, 3e8 / (k * d))))
+    xb, _ = orc.make_blobs_rows(0, probe, d, n_blobs, seed=0)
     t0 = time.perf_counter()
     orc.partial_sum(xb, centers)
     rate1 = probe / (time.perf_counter() - t0)
-    rows_per_task = 25_000
+    rows_per_task = int(max(16, min(25_000, rate1 * 0.5)))
     n_tasks = max(cores, int(rate1 * cores * target_s / rows_per_task))
-    tasks = [(i * rows_per_task, rows_per_task, d, k) for i in range(n_tasks)]
+    tasks = [(i * rows_per_task, rows_per_task, d, n_blobs)
+             for i in range(n_tasks)]
     ctx = mp.get_context("fork")
     with ctx.Pool(cores) as pool:
         pool.map(_cpu_gen, tasks[:cores])          # warm the workers
@@ -83,26 +107,33 @@ def cpu_baseline(d, k, target_s, centers):
         el = time.perf_counter() - t0
     n = n_tasks * rows_per_task
     # faithful per-sample-loop variant (the reference's own cost model)
-    xs, _ = orc.make_blobs_rows(0, 2000, d, k, seed=0)
+    m = int(max(4, min(2000, rate1 * 0.02)))
+    xs, _ = orc.make_blobs_rows(0, m, d, n_blobs, seed=0)
     t0 = time.perf_counter()
     for s in xs:
         np.argmin(orc.vec_matrix_euclid(s, centers))
-    faithful = 2000 / (time.perf_counter() - t0)
+    faithful = m / (time.perf_counter() - t0)
     return {"value": n / el, "unit": "samples·iters/s", "cores": cores,
             "kind": "port",
             "sample": "%d rows (%d Subsets of %d) of the same make_blobs "
                       "workload, one Lloyd iteration (distances+argmin+"
                       "sums+arity-50 merge), vectorised numpy oracle, one "
-                      "process per core, BLAS threads 1" %
-                      (n, n_tasks, rows_per_task),
+                      "process per core of this job's CPU share, BLAS "
+                      "threads 1" % (n, n_tasks, rows_per_task),
             "seconds": el,
+            "per_core": n / el / cores,
+            "machine_threads": machine,
+            "note": "cores = the CPU share the GPU box grants one GPU's job "
+                    "(OMP_NUM_THREADS); the oracle scales linearly over "
+                    "Subsets, so per_core x machine_threads bounds a "
+                    "whole-machine run",
             "faithful_per_sample_loop_1core": faithful}
 
 
 def _cpu_gen(args):
     from oracle import kmeans_oracle as orc
-    row0, n, d, k = args
-    return orc.make_blobs_rows(row0, n, d, k, seed=0)[0]
+    row0, n, d, nb = args
+    return orc.make_blobs_rows(row0, n, d, nb, seed=0)[0]
 
 
 def _cpu_task(block, centers):
@@ -111,51 +142,32 @@ def _cpu_task(block, centers):
     return (s, c)
 
 
-def main():
-    a = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-
-    # CPU baseline first, before anything touches the GPU: its worker pool is
-    # forked from a process with no HIP state and is gone before GPU init.
-    cpu = None
-    if world == 1 and not a.no_cpu:
-        from dislib_amd.cluster.kmeans import _init_centers as _ic
-        cpu = cpu_baseline(a.d, a.k, a.cpu_seconds, _ic(a.d, False, a.k, 0))
-
-    import torch
-    import torch.distributed as dist
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-
-    from dislib_amd import _device, _lib
+# ---------------------------------------------------------------------------
+# one configuration on the GPU(s)
+# ---------------------------------------------------------------------------
+def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
+               mode, labels, n_blobs=None):
+    from dislib_amd import _device, _shard
     from dislib_amd.cluster.kmeans import _Lloyd, _init_centers
     from dislib_amd.data import Dataset, Subset
-
-    n, d, k = a.n, a.d, a.k
+    n_blobs = n_blobs or k
     X = torch.empty((n, d), dtype=torch.float64, device=dev)
     # global rows [rank*n, (rank+1)*n): the ranks shard one dataset
-    _device.make_blobs(X, rank * n, k, seed=0, box=10.0, std=1.0)
+    _device.make_blobs(X, rank * n, n_blobs, seed=0, box=10.0, std=1.0)
     ds = Dataset(n_features=d)
-    for i in range(0, n, a.subset):
-        ds.append(Subset(X[i:i + a.subset]))
-    centers0 = _init_centers(d, False, k, 0)
-    st = _Lloyd(ds, centers0, 0.0, a.labels, a.mode, dev)
+    for i in range(0, n, subset):
+        ds.append(Subset(X[i:i + subset]))
+    st = _Lloyd(ds, _init_centers(d, False, k, 0), 0.0, labels, mode, dev)
     torch.cuda.synchronize()
-
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         st.step()
-
     ev = [(torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+           torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
+    for i in range(steps):
         st.prepare()
         ev[i][0].record()
         st.partial()                  # the dominant kernel(s), same stream
@@ -171,29 +183,122 @@ def main():
         t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
-    rechecked = st.rechecked()
+    out = {"el": el, "kern_ms": kern_ms, "rechecked": st.rechecked(),
+           "collective": ("libdkm-rccl" if _shard._COMM else
+                          "torch.distributed") if world > 1 else "none"}
+    del st, ds, X
+    torch.cuda.empty_cache()
+    return out
+
+
+def roofline(n, d, k, r, labels):
+    """Roofline of the assignment call (the dominant kernels).  Small d:
+    HBM-bound, algorithmic bytes = X read (8 d) + labels (delta path:
+    previous label read 4 B + label write 4 B).  d > 128: MFMA-bound, the
+    executed bf16x3 MFMA flops of the GEMM screen (3 products x 2 k d per
+    sample over the padded tiles) against the dense bf16 peak."""
+    sec = r["kern_ms"] * 1e-3
+    if d <= 128:
+        b = n * (8 * d + 8)
+        out = {"bound": "hbm", "achieved": b / sec / 1e9,
+               "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": b / sec / 1e9 / HBM_PEAK_GBS,
+               "bytes_per_sample": 8 * d + 8,
+               "kernel": "dkm_assign_delta / dkm_partial_sum (screen + "
+                         "re-check)",
+               "kernel_ms": r["kern_ms"],
+               # bf16x3: 3 MFMA products per x.c term
+               "mfma_bf16_tflops_executed": 6.0 * k * d * n / sec / 1e12,
+               "mfma_bf16_peak_tflops": BF16_PEAK_TFLOPS}
+    else:
+        dp, kp = (d + 31) // 32 * 32, (k + 255) // 256 * 256
+        f = 6.0 * kp * dp * n
+        out = {"bound": "mfma", "achieved": f / sec / 1e12,
+               "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+               "frac": f / sec / 1e12 / BF16_PEAK_TFLOPS,
+               "kernel": "dkm_assign (bf16x3 GEMM screen + exact "
+                         "candidates + sums)",
+               "kernel_ms": r["kern_ms"],
+               "alg_fp64_equiv_tflops": 2.0 * k * d * n / sec / 1e12,
+               "fp64_peak_tflops": FP64_PEAK_TFLOPS,
+               "hbm_gbs": n * 8 * d / sec / 1e9}
+    out["traffic"] = None
+    return out
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    extras = [] if a.only_headline else [
+        # (name, n, d, k, subset, steps, warmup)
+        ("KMeans k=1000 on 125M x 64 fp64 dense per GPU (BASELINE "
+         "configs[2] per-GPU shard; north-star target)",
+         125_000_000, 64, 1000, 1_000_000, 10, 2),
+        ("KMeans k=4096 on 10M x 1024 fp64 dense per GPU (BASELINE "
+         "configs[3], MFMA-bound)", 10_000_000, 1024, 4096, 1_000_000, 5, 3),
+    ]
+
+    # CPU baselines first, before anything touches the GPU: their worker
+    # pools are forked from a process with no HIP state and are gone before
+    # GPU init.
+    cpu = {}
+    if world == 1 and not a.no_cpu:
+        from dislib_amd.cluster.kmeans import _init_centers as _ic
+        cpu["head"] = cpu_baseline(a.d, a.k, a.cpu_seconds,
+                                   _ic(a.d, False, a.k, 0), a.k)
+        for i, (_, n, d, k, *_r) in enumerate(extras):
+            cpu[i] = cpu_baseline(d, k, a.cpu_seconds / 2,
+                                  _ic(d, False, k, 0), k)
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    r = run_config(torch, dist, dev, rank, world, a.n, a.d, a.k, a.subset,
+                   a.steps, a.warmup, a.mode, a.labels)
+    fp = None
+    if not a.only_headline and not a.labels:
+        fp = run_config(torch, dist, dev, rank, world, a.n, a.d, a.k,
+                        a.subset, a.steps, a.warmup, a.mode, True)
+    ex = []
+    for i, (name, n, d, k, sub, steps, warm) in enumerate(extras):
+        rr = run_config(torch, dist, dev, rank, world, n, d, k, sub, steps,
+                        warm, a.mode, False)
+        e = {"workload": name, "n_per_gpu": n, "d": d, "k": k,
+             "value": n * world * steps / rr["el"],
+             "unit": "samples·iters/s", "ms_per_step": rr["el"] / steps * 1e3,
+             "steps": steps, "warmup": warm,
+             "roofline": roofline(n, d, k, rr, False),
+             "rechecked_samples": rr["rechecked"]}
+        if i in cpu:
+            cpu[i]["gpu_over_cpu"] = e["value"] / cpu[i]["value"]
+            e["cpu_baseline"] = cpu[i]
+        ex.append(e)
 
     if rank != 0:
+        from dislib_amd import _shard
+        _shard.finalize()
         if world > 1:
             dist.destroy_process_group()
         return
 
-    total = n * world * a.steps
-    value = total / el
-    bytes_per_launch = n * d * 8 + (n * 4 if a.labels else 0)
-    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    flops = 2.0 * k * d * n
-    # HBM bytes per launch from the committed PMC passes (tools/pmc_session.sh
-    # -> tools/pmc_summary.py --traffic-out), scaled to this launch's rows
-    traffic = None
+    value = a.n * world * a.steps / r["el"]
+    rf = roofline(a.n, a.d, a.k, r, a.labels)
     if os.path.exists(a.traffic_json):
+        # HBM bytes per launch from the committed PMC passes
+        # (tools/pmc_session.sh -> tools/pmc_summary.py --traffic-out)
         try:
             tj = json.load(open(a.traffic_json))
-            if tj.get("d") == d and tj.get("k") == k:
-                traffic = n * (tj["hbm_read_bytes_per_sample"] +
-                               tj["hbm_write_bytes_per_sample"])
+            if tj.get("d") == a.d and tj.get("k") == a.k:
+                rf["traffic"] = a.n * (tj["hbm_read_bytes_per_sample"] +
+                                       tj["hbm_write_bytes_per_sample"])
         except (OSError, ValueError, KeyError):
-            traffic = None
+            pass
     out = {
         "metric": METRIC,
         "value": value,
@@ -201,30 +306,36 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": el / a.steps * 1e3,
+        "ms_per_step": r["el"] / a.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (on-device counter-based make_blobs, 100 blobs)",
+        "data": "synthetic (on-device counter-based make_blobs, k blobs)",
         "config": {"workload": "KMeans k=%d on %dM x %d fp64 dense per GPU "
-                               "(BASELINE configs[1])" % (k, n // 10**6, d),
-                   "n_per_gpu": n, "d": d, "k": k, "subset_size": a.subset,
-                   "mode": a.mode, "labels": bool(a.labels),
+                               "(BASELINE configs[1])" % (a.k, a.n // 10**6,
+                                                          a.d),
+                   "n_per_gpu": a.n, "d": a.d, "k": a.k,
+                   "subset_size": a.subset, "mode": a.mode,
+                   "labels": bool(a.labels),
                    "parallelism": "dp%d" % world},
-        "roofline": {"bound": "hbm", "achieved": achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "dkm_partial_sum (k_screen + k_recheck)",
-                     "kernel_ms": kern_ms,
-                     "fp32_screen_tflops": flops / (kern_ms * 1e-3) / 1e12,
-                     "fp32_peak_tflops": FP32_PEAK_TFLOPS},
-        "rechecked_samples": rechecked,
+        "roofline": rf,
+        "rechecked_samples": r["rechecked"],
+        "collective": r["collective"],
     }
-    if cpu is not None:
-        cpu["gpu_over_cpu"] = value / cpu["value"]
-        out["cpu_baseline"] = cpu
+    if fp is not None:
+        out["fit_predict"] = {
+            "value": a.n * world * a.steps / fp["el"],
+            "ms_per_step": fp["el"] / a.steps * 1e3,
+            "roofline": roofline(a.n, a.d, a.k, fp, True)}
+    if "head" in cpu:
+        cpu["head"]["gpu_over_cpu"] = value / cpu["head"]["value"]
+        out["cpu_baseline"] = cpu["head"]
+    if ex:
+        out["extra_configs"] = ex
     print(json.dumps(out), flush=True)
+    from dislib_amd import _shard
+    _shard.finalize()
     if world > 1:
         dist.destroy_process_group()
 

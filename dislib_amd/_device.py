@@ -28,6 +28,25 @@ def stream_ptr():
     return ctypes.c_void_p(t.cuda.current_stream().cuda_stream)
 
 
+def resolve(device=None):
+    """A concrete ``torch.device('cuda', i)``: ``None`` / ``'cuda'`` mean the
+    current device, so a fit keeps using the GPU it started on."""
+    t = torch()
+    dev = t.device(device if device is not None else "cuda")
+    if dev.type != "cuda":
+        raise ValueError("dislib_amd runs on a ROCm GPU, got device %s" % dev)
+    if dev.index is None:
+        dev = t.device("cuda", t.cuda.current_device())
+    return dev
+
+
+def on(device):
+    """Context in which launches go to ``device``: HIP launches and
+    ``stream_ptr()`` use the current device, so every entry point that
+    touches the data of a Dataset runs inside ``with on(dd.device):``."""
+    return torch().cuda.device(device)
+
+
 def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -36,8 +55,7 @@ class DeviceData:
     """HBM image of a Dataset (dense or CSR)."""
 
     def __init__(self, dataset, device=None):
-        t = torch()
-        self.device = t.device(device if device is not None else "cuda")
+        self.device = resolve(device)
         subsets = list(dataset)
         self.sizes = [int(s.samples.shape[0]) for s in subsets]
         self.offsets = np.concatenate([[0], np.cumsum(self.sizes)]).astype(

@@ -15,6 +15,7 @@ ABI_VERSION = 1
 MODE_AUTO, MODE_EXACT, MODE_SCREEN32, MODE_BF16X3 = 0, 1, 2, 3
 SUMS_F64, SUMS_F32, SUMS_RECIP = 0, 1, 2
 PREP_CSR = 1
+COMM_ID_BYTES = 128
 
 _p = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -51,6 +52,12 @@ SIGNATURES = {
     "dkm_make_blobs_f64": (_i32, [_p, _i64, _i64, _i64, _i64, _u64, _f64,
                                   _f64, _p, _p]),
     "dkm_screen_stats": (_i32, [_p, ctypes.POINTER(_i64), _p]),
+    # multi-GPU all-reduce (RCCL)
+    "dkm_allreduce_unique_id": (_i32, [_p]),
+    "dkm_allreduce_init_rank": (_i32, [ctypes.c_char_p, _i32, _i32, _i32]),
+    "dkm_allreduce_init": (_i32, [_i32, ctypes.POINTER(_i32)]),
+    "dkm_allreduce_sum_f64": (_i32, [_p, _i64, _i32, _p]),
+    "dkm_allreduce_finalize": (_i32, []),
     # host-side loaders (no GPU)
     "dkm_libsvm_count": (_i32, [_p, _i64, _i32, _p]),
     "dkm_libsvm_parse": (_i32, [_p, _i64, _i32, _p, _p, _p, _p, _p]),

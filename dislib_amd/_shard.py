@@ -7,8 +7,13 @@ plus the ``_merge`` arity tree (``cluster/kmeans/base.py:113-117, 137-143,
 * every rank owns a contiguous block of whole Subsets (:func:`shard_range`),
 * every rank computes [sums | counts] of its samples into one packed fp64
   buffer of k*(d+1) values (:mod:`dislib_amd._device`),
-* ``torch.distributed.all_reduce(SUM)`` -- RCCL over xGMI for the ``nccl``
-  backend -- gives every rank the global buffer,
+* one in-place RCCL all-reduce (SUM) over xGMI through libdkm's C ABI
+  (``dkm_allreduce_sum_f64``, ``dislib_amd/csrc/dkm_comm.cpp``) gives every
+  rank the global buffer -- under a ``nccl`` process group the library's
+  own communicator is brought up on first use (the 128-byte RCCL id goes
+  from rank 0 to the others through ``torch.distributed``, which is only
+  the rendezvous); under ``gloo`` (CPU tests, or several ranks sharing one
+  GPU) the same reduction runs through ``torch.distributed.all_reduce``,
 * every rank runs the identical centre update, so the centres and the
   convergence decision are replicated without a broadcast.
 
@@ -57,11 +62,63 @@ def shard_dataset(dataset, rank=None, world_size=None):
     return out
 
 
+_COMM = {}   # device index -> True once libdkm's RCCL communicator is up
+
+
+def _dkm_comm(t, d):
+    """libdkm's RCCL communicator for ``t``'s device, brought up on first
+    use (every rank reaches its first all-reduce together).  None when the
+    group is not ``nccl`` or ``t`` is not a GPU tensor."""
+    import ctypes
+
+    from . import _lib
+    if d.get_backend() != "nccl" or not t.is_cuda:
+        return None
+    dev = t.device.index
+    if dev in _COMM:
+        return dev
+    so = _lib.lib()
+    rank, world = d.get_rank(), d.get_world_size()
+    buf = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
+    if rank == 0:
+        _lib.check(so.dkm_allreduce_unique_id(buf), "dkm_allreduce_unique_id")
+    obj = [bytes(buf.raw) if rank == 0 else None]
+    d.broadcast_object_list(obj, src=0)
+    _lib.check(so.dkm_allreduce_init_rank(obj[0], world, rank, dev),
+               "dkm_allreduce_init_rank")
+    _COMM[dev] = True
+    return dev
+
+
+def finalize():
+    """Destroy libdkm's RCCL communicators (before the process group)."""
+    if _COMM:
+        from . import _lib
+        _lib.check(_lib.lib().dkm_allreduce_finalize(),
+                   "dkm_allreduce_finalize")
+        _COMM.clear()
+
+
 def allreduce_sum_(t):
-    """In-place SUM over all ranks (RCCL for CUDA tensors on ``nccl``)."""
+    """In-place SUM of a contiguous fp64 buffer over all ranks."""
     d = _dist()
-    if d is not None and d.get_world_size() > 1:
+    if d is None or d.get_world_size() == 1:
+        return t
+    dev = _dkm_comm(t, d)
+    if dev is None:
         d.all_reduce(t, op=d.ReduceOp.SUM)
+        return t
+    import ctypes
+
+    import torch
+
+    from . import _lib
+    if t.dtype != torch.float64 or not t.is_contiguous():
+        raise ValueError("allreduce_sum_: contiguous float64 buffer expected")
+    _lib.check(_lib.lib().dkm_allreduce_sum_f64(
+        ctypes.c_void_p(t.data_ptr()), t.numel(), dev,
+        ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)),
+        "dkm_allreduce_sum_f64")
     return t
 
 
@@ -70,6 +127,19 @@ def broadcast_(t, src=0):
     if d is not None and d.get_world_size() > 1:
         d.broadcast(t, src=src)
     return t
+
+
+def broadcast_int(value, device=None):
+    """Rank 0's integer on every rank (the value itself when not
+    distributed).  ``device``: where the collective runs (nccl: the GPU)."""
+    d = _dist()
+    if d is None or d.get_world_size() == 1:
+        return int(value)
+    import torch
+    dev = device if d.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+    d.broadcast(t, src=0)
+    return int(t[0])
 
 
 def agree(flag_value):

@@ -86,12 +86,16 @@ class KMeans:
         """Set each sample's label to its closest centre."""
         if self.centers is None:
             raise ValueError("KMeans.predict before fit")
-        from .._device import Workspace, predict, prepare, torch
+        from .._device import Workspace, on, predict, prepare, torch
         t = torch()
         _lib.lib()
         dd = dataset._device_data(self._device)
         if dd.n == 0:
             return
+        with on(dd.device):
+            self._predict_on(dataset, dd, t, Workspace, predict, prepare)
+
+    def _predict_on(self, dataset, dd, t, Workspace, predict, prepare):
         centers = self.centers.toarray() if issparse(self.centers) else \
             np.asarray(self.centers, dtype=np.float64)
         k, d = centers.shape
@@ -134,6 +138,11 @@ class KMeans:
         state.attach_labels()
 
 
+# Full recomputation of the running [sums | counts] every REFRESH
+# iterations (1 = every iteration).  Between refreshes the delta updates
+# add rounding of at most REFRESH * 2^-52 * (|S_old| + |moved rows|) per
+# sum element (a shrinking cluster keeps the error of its larger past
+# sums); the fit tests pin the centres at 1e-9 of the oracle with 8.
 REFRESH = int(os.environ.get("DKM_REFRESH", "8"))
 
 
@@ -152,10 +161,11 @@ class _Lloyd:
 
     def __init__(self, dataset, centers, tol, set_labels, mode="auto",
                  device=None, broadcast_init=False):
-        from .._device import Workspace, torch
+        from .._device import Workspace, on, torch
         t = torch()
         self.dataset = dataset
         self.dd = dd = dataset._device_data(device)
+        self._on = lambda: on(dd.device)
         self.sparse = dd.sparse
         k, d = centers.shape
         if d != dd.d:
@@ -182,14 +192,20 @@ class _Lloyd:
             self.sums_mode = _lib.SUMS_F64
         self.mode = _MODES[mode]
         self.tol = tol
+        if REFRESH < 1:
+            raise ValueError("DKM_REFRESH must be >= 1, got %d" % REFRESH)
+        # every rank must refresh on the same iterations (their delta states
+        # are summed): rank 0's setting wins
+        self.refresh = _shard.broadcast_int(REFRESH, dd.device)
 
     def prepare(self):
         """Per-iteration centre data + zeroed accumulator."""
         from .._device import prepare
-        prepare(self.C, self.ws, self.acc, csr=self.sparse)
+        with self._on():
+            prepare(self.C, self.ws, self.acc, csr=self.sparse)
 
     def _full(self):
-        return self.sparse or self.it % REFRESH == 0
+        return self.sparse or self.it % self.refresh == 0
 
     def partial(self):
         """The hot kernel: fused assignment over all resident samples, full
@@ -198,12 +214,13 @@ class _Lloyd:
         from .._device import assign_delta, partial_sum
         if self.dd.n == 0:
             return
-        if self._full():
-            partial_sum(self.dd, self.C, self.ws, self.labels, self.acc,
-                        self.mode)
-        else:
-            assign_delta(self.dd, self.C, self.ws, self.labels, self.acc,
-                         self.mode)
+        with self._on():
+            if self._full():
+                partial_sum(self.dd, self.C, self.ws, self.labels, self.acc,
+                            self.mode)
+            else:
+                assign_delta(self.dd, self.C, self.ws, self.labels, self.acc,
+                             self.mode)
 
     def assign(self):
         self.prepare()
@@ -211,13 +228,14 @@ class _Lloyd:
 
     def reduce_update(self):
         from .._device import add_, update
-        _shard.allreduce_sum_(self.acc)
-        if self._full():
-            self.state.copy_(self.acc)
-        else:
-            add_(self.state, self.acc)
-        update(self.state, self.C, self.sums_mode, self.tol, self.diff,
-               self.flag)
+        with self._on():
+            _shard.allreduce_sum_(self.acc)
+            if self._full():
+                self.state.copy_(self.acc)
+            else:
+                add_(self.state, self.acc)
+            update(self.state, self.C, self.sums_mode, self.tol, self.diff,
+                   self.flag)
         self.it += 1
 
     def step(self):
@@ -230,7 +248,8 @@ class _Lloyd:
 
     def rechecked(self):
         from .._device import rechecked
-        return 0 if self.sparse else rechecked(self.ws)
+        with self._on():
+            return 0 if self.sparse else rechecked(self.ws)
 
     def centers_host(self):
         return self.C.cpu().numpy()

@@ -85,13 +85,13 @@ static DevInfo dev_info() {
 // ~100-SGPR kernels here), the LDS limit (160 KiB per CU) and 32 waves per
 // CU (MI355X_MICROARCH.md "Register files", "Residency").  The occupancy
 // API answered 1 for the 512-thread screen where 3 fit (2 instead of 6
-// waves per SIMD), so it is not used.  DKM_BLOCKS_PER_CU overrides, and
-// DKM_VERBOSE prints the numbers.
+// waves per SIMD), so it is not used.  A/B builds (variants.sh) may pin the
+// count with -DDKM_AB_BLOCKS_PER_CU=n and print the numbers with
+// -DDKM_AB_VERBOSE; the product build has neither.
 static int resident_blocks(const void *kf, int block, size_t lds) {
-  if (const char *e = getenv("DKM_BLOCKS_PER_CU")) {
-    const int v = atoi(e);
-    if (v > 0) return v;
-  }
+#ifdef DKM_AB_BLOCKS_PER_CU
+  return DKM_AB_BLOCKS_PER_CU;
+#endif
   hipFuncAttributes fa;
   if (hipFuncGetAttributes(&fa, kf) != hipSuccess) return 1;
   const int waves = (block + 63) / 64;
@@ -102,7 +102,8 @@ static int resident_blocks(const void *kf, int block, size_t lds) {
   const int by_lds = l ? (int)(LDS_PER_CU / l) : 32;
   const int own =
       std::max(1, std::min(std::min(by_regs, by_lds), 32 / waves));
-  if (getenv("DKM_VERBOSE")) {
+#ifdef DKM_AB_VERBOSE
+  {
     int api = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&api, kf, block, lds) !=
         hipSuccess)
@@ -110,6 +111,7 @@ static int resident_blocks(const void *kf, int block, size_t lds) {
     fprintf(stderr, "dkm: block %d lds %zu vgpr %d -> %d/CU (api %d)\n",
             block, l, fa.numRegs, own, api);
   }
+#endif
   return own;
 }
 
@@ -479,6 +481,24 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
   __attribute__((amdgpu_waves_per_eu( \
       DKM_WPE <= 0 ? 1 : (NKS) == 1 ? DKM_WPE : (NKS) == 2 ? 4 : 1)))
 constexpr int SB = DKM_SB;  // screen block: SB/64 waves share one LDS image
+
+// A/B switches, compile-time only (variants.sh -DDKM_AB_...=1; all off in the
+// product build): no W32 screen, delta sums always / never by k_label_sums,
+// no per-wave undecided lists.
+#ifndef DKM_AB_NO_W32
+#define DKM_AB_NO_W32 0
+#endif
+#ifndef DKM_AB_DELTA_POST
+#define DKM_AB_DELTA_POST 0
+#endif
+#ifndef DKM_AB_NO_POST
+#define DKM_AB_NO_POST 0
+#endif
+#ifndef DKM_AB_NO_LIST
+#define DKM_AB_NO_LIST 0
+#endif
+constexpr bool AB_NO_W32 = DKM_AB_NO_W32, AB_DELTA_POST = DKM_AB_DELTA_POST,
+               AB_NO_POST = DKM_AB_NO_POST, AB_NO_LIST = DKM_AB_NO_LIST;
 
 // Eight consecutive features t0..t0+7 of one row, as fp64.  VEC: d % 8 == 0
 // and 16-B aligned rows, so the 8 features are in range iff t0 < d.
@@ -1937,7 +1957,7 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const size_t fb32 = (size_t)(kpad32(k) / 32) * (4096 + 128);
   const bool w32 = prec == P_B3 && d <= 32 && vec && fb32 <= LDS_BUDGET &&
                    (int64_t)32 * ldx * (int64_t)sizeof(TX) < (1ll << 31) &&
-                   !getenv("DKM_NO_W32");
+                   !AB_NO_W32;
   const int chb = w32 ? 0 : screen_chunk_blocks(k, d);
   const size_t fb = w32 ? fb32
                     : chb ? (size_t)chb * ((dpad32(d) / 32) * 2048 + 64)
@@ -1947,11 +1967,11 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   // and k_label_sums accumulates from them (delta: against a copy of the
   // previous labels in the label scratch)
   const bool lds_fits = fb + a_bytes <= LDS_BUDGET;
-  // DKM_DELTA_POST: delta sums from k_label_sums even when they fit LDS
+  // AB_DELTA_POST: delta sums from k_label_sums even when they fit LDS
   // (the screen then needs only the fragments' LDS: more blocks per CU)
-  const bool force_post = acc_kind == 2 && getenv("DKM_DELTA_POST");
+  const bool force_post = acc_kind == 2 && AB_DELTA_POST;
   const bool post = acc_kind != 0 && (!lds_fits || force_post) &&
-                    !getenv("DKM_NO_POST") &&
+                    !AB_NO_POST &&
                     (acc_kind == 1 || (labels && nq >= n));
   const int32_t *prevbuf = nullptr;
   if (post && acc_kind == 2) {
@@ -1963,7 +1983,7 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const int skind = post ? 0 : acc_kind;
   const int amode = acc_mode(skind, lds_fits);
   const size_t lds = fb + ((amode & AM_INLDS) ? a_bytes : 0);
-  const int use_list = list_ok(k, d) && !getenv("DKM_NO_LIST") ? 1 : 0;
+  const int use_list = list_ok(k, d) && !AB_NO_LIST ? 1 : 0;
   for (int64_t base = 0; base < n; base += chunk) {
     const int64_t end = std::min(n, base + chunk);
     int32_t *lab_out = labels ? labels : v.queue - base;

@@ -27,6 +27,11 @@
 
 #include "dkm_internal.h"
 
+// A/B switch (variants.sh): the per-centre-group kernel for every k
+#ifndef DKM_AB_CSR_OLD
+#define DKM_AB_CSR_OLD 0
+#endif
+
 namespace dkm {
 
 __global__ void __launch_bounds__(256)
@@ -164,7 +169,7 @@ static int csr_assign(const int64_t *indptr, const int32_t *indices,
 #define DKM_CSR_R(KPL)                                                       \
   k_csr_assign_r<KPL><<<g, 256, 0, s>>>(indptr, indices, data, n, (int)d,     \
                                         v.ct64, v.cn64, (int)k, labels, acc)
-  if (getenv("DKM_CSR_OLD") || k > 512)
+  if (DKM_AB_CSR_OLD || k > 512)
     k_csr_assign<<<g, 256, 0, s>>>(indptr, indices, data, n, (int)d, v.ct64,
                                    v.cn64, (int)k, labels, acc);
   else if (k <= 64)

@@ -1,12 +1,16 @@
 #!/bin/bash
 # Build A/B variants of libdkm.so (screen-kernel compile-time knobs) next to
 # the default library: ../libdkm_<name>.so.  usage: bash variants.sh name "DEFS" ...
+# A/B switches are compile-time only (-DDKM_AB_NO_W32=1, -DDKM_AB_DELTA_POST=1,
+# -DDKM_AB_NO_POST=1, -DDKM_AB_NO_LIST=1, -DDKM_AB_CSR_OLD=1,
+# -DDKM_AB_BLOCKS_PER_CU=n, -DDKM_AB_VERBOSE): the product build reads no
+# environment variable.
 set -e
 cd "$(dirname "$0")"
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
   d=build_$name; mkdir -p $d
-  for f in dkm_util dkm_dense dkm_sparse; do
+  for f in dkm_util dkm_dense dkm_sparse dkm_gemm; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off \
       -fno-slp-vectorize $defs -c $f.hip -o $d/$f.o &
   done

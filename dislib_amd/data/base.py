@@ -187,7 +187,15 @@ def _load_file(path, subset_size, fmt, n_features, delimiter=None,
     if fmt == "libsvm":
         n_lines, indptr, indices, data, y, row_line = parse_libsvm(buf)
     else:
-        n_lines, vals, row_line = parse_txt(buf, delimiter)
+        try:
+            n_lines, vals, row_line = parse_txt(buf, delimiter)
+        except ValueError as e:
+            if "columns instead of" not in str(e):
+                raise
+            # rows of different widths: genfromtxt runs per chunk in the
+            # reference, so a width may change from one chunk to the next
+            return _load_txt_chunks(buf, subset_size, n_features, delimiter,
+                                    label_col)
     n_chunks = -(-n_lines // subset_size)
     bounds = np.searchsorted(row_line, np.arange(n_chunks + 1) * subset_size)
     image = []
@@ -202,8 +210,23 @@ def _load_file(path, subset_size, fmt, n_features, delimiter=None,
             dataset.append(_txt_subset(vals[r0:r1], label_col))
     if fmt == "libsvm" and image:
         # concatenated host image for the one-shot HBM upload
-        dataset._host_image = sp.vstack(image, format="csr") if \
-            store_sparse else None
+        if store_sparse:
+            dataset._set_host_image(sp.vstack(image, format="csr"))
+    return dataset
+
+
+def _load_txt_chunks(buf, subset_size, n_features, delimiter, label_col):
+    """Text file whose rows differ in width: parse each chunk of
+    ``subset_size`` raw lines on its own, exactly as the reference's
+    per-chunk ``np.genfromtxt`` (``data/base.py:150-164, 183-188``); a
+    width change inside one chunk raises ValueError there too.  Lines end
+    at \\n, \\r\\n or \\r (Python text mode, like ``bytes.splitlines``)."""
+    dataset = Dataset(n_features, False)
+    lines = buf.splitlines(keepends=True)
+    for c0 in range(0, len(lines), subset_size):
+        chunk = b"".join(lines[c0:c0 + subset_size])
+        _, vals, _ = parse_txt(chunk, delimiter)
+        dataset.append(_txt_subset(vals, label_col))
     return dataset
 
 

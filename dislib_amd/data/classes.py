@@ -130,6 +130,7 @@ class Dataset(object):
         self._sparse = sparse
         self._device = None        # DeviceData cache
         self._host_image = None    # loader's concatenated CSR (one upload)
+        self._host_image_sig = None
 
     def __getitem__(self, item):
         return self._subsets.__getitem__(item)
@@ -232,11 +233,35 @@ class Dataset(object):
                 self._samples = concat_f((self._samples, s.samples))
 
     # -- device residency --------------------------------------------------
+    def _signature(self):
+        """Identity of the Subsets' sample objects: any reassignment
+        (``ds[i].samples = ...``, ``Subset.concatenate``, a new Subset)
+        changes it.  In-place writes into a sample array keep it -- the
+        HBM image is then stale; re-assign the array to refresh it."""
+        return tuple((id(s.samples), tuple(s.samples.shape))
+                     for s in self._subsets)
+
     def _device_data(self, device=None):
-        from .._device import DeviceData
-        if self._device is None:
-            self._device = DeviceData(self, device)
-        return self._device
+        """The HBM image of the samples, rebuilt when the Subsets' sample
+        objects or the requested device changed since the upload (the
+        reference reads Subset samples afresh on every call)."""
+        from .._device import DeviceData, resolve
+        dev = resolve(device) if device is not None else None
+        sig = self._signature()
+        dd = self._device
+        if dd is None or dd.signature != sig or \
+                (dev is not None and dd.device != dev):
+            if self._host_image is not None and \
+                    self._host_image_sig != sig:
+                self._host_image = None     # loader image of other samples
+            dd = DeviceData(self, device)
+            dd.signature = sig
+            self._device = dd
+        return dd
+
+    def _set_host_image(self, image):
+        self._host_image = image
+        self._host_image_sig = self._signature()
 
     def _attach_device_labels(self, labels_tensor):
         src = _DeviceLabels(labels_tensor)

@@ -36,6 +36,7 @@ extern "C" {
 #define DKM_E_WORKSPACE 10002 /* workspace too small                         */
 #define DKM_E_LAUNCH 10003    /* kernel launch failed                        */
 #define DKM_E_PARSE 10004     /* malformed input text (loaders)              */
+#define DKM_E_COMM 10005      /* RCCL missing or an RCCL call failed         */
 
 /* assignment modes (flags) */
 #define DKM_MODE_AUTO 0     /* library picks: SCREEN32 when profitable       */
@@ -144,6 +145,29 @@ int dkm_predict_csr_f64(const int64_t *indptr, const int32_t *indices,
                         const double *data, int64_t n, int64_t d,
                         const double *C, int64_t k, const void *ws,
                         size_t ws_bytes, int32_t *labels, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Multi-GPU: the one collective of a Lloyd iteration (SURVEY.md section
+ * 8(b,e)).  Replaces the `_merge` arity tree and the `compss_wait_on` gather
+ * (cluster/kmeans/base.py:137-143, 184-191): an in-place RCCL sum of every
+ * GPU's [sums k*d | counts k] buffer; each rank then runs the same
+ * dkm_update_centers.  librccl is loaded at the first call (the instance
+ * already in the process if any).  Host functions.
+ * --------------------------------------------------------------------- */
+#define DKM_COMM_ID_BYTES 128
+
+/* One process per GPU: rank 0 creates the id (DKM_COMM_ID_BYTES bytes),
+ * the caller hands it to every rank, every rank joins with its device. */
+int dkm_allreduce_unique_id(void *id);
+int dkm_allreduce_init_rank(const void *id, int nranks, int rank, int device);
+/* One process driving ndev GPUs (ncclCommInitAll over devs[]). */
+int dkm_allreduce_init(int ndev, const int *devs);
+/* buf[0..count) (device memory of `device`) <- sum over all ranks,
+ * stream-ordered on `stream` (a hipStream_t of that device). */
+int dkm_allreduce_sum_f64(double *buf, int64_t count, int device,
+                          void *stream);
+/* Destroy every communicator of this process. */
+int dkm_allreduce_finalize(void);
 
 /* Synthetic make_blobs rows [row0, row0+n) into X (n x d, ld = d), blob ids
  * into blob (nullable).  Counter-based: any row range regenerates

@@ -1,0 +1,77 @@
+"""One rank of a multi-process KMeans fit on the GPU, started by
+tests/test_gpu_dist.py through torch.distributed.run (not a test module).
+
+Every rank builds the same seeded dataset, takes its contiguous block of
+Subsets (``shard_dataset``), runs the product ``KMeans.fit_predict`` (HIP
+kernels, per-iteration all-reduce of [sums | counts]) and writes its
+centres, n_iter, labels and initial centres to ``<out>.<rank>.npz``.
+Several ranks share one GPU here, so the group is ``gloo`` (RCCL refuses
+two ranks on one device); the collective is the same ``_shard`` entry point
+the ``nccl`` path takes.
+
+  python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1
+      --master-port P tests/dist_worker.py --case NAME --out PREFIX
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CASES = {
+    # name: (n, d, blobs, k, subset, max_iter, tol, random_state, refresh)
+    "dense": (24000, 16, 12, 12, 1000, 12, 0.0, 0, 3),
+    "gemm": (6000, 200, 20, 40, 500, 4, 0.0, 3, 2),
+    "none": (9000, 8, 6, 6, 1000, 8, 1e-6, None, 8),
+    "ragged": (7001, 24, 9, 9, 700, 5, 0.0, 5, 8),
+}
+
+
+def data(case):
+    from sklearn.datasets import make_blobs
+    n, d, blobs = CASES[case][:3]
+    x, _ = make_blobs(n_samples=n, n_features=d, centers=blobs,
+                      center_box=(-8, 8), random_state=42)
+    return x
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--case", required=True)
+    p.add_argument("--out", required=True)
+    a = p.parse_args()
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ["RANK"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    import dislib_amd.cluster.kmeans as km_mod
+    from dislib_amd import shard_dataset
+    from dislib_amd.cluster import KMeans
+    from dislib_amd.data import load_data
+    n, d, blobs, k, sub, iters, tol, rs, refresh = CASES[a.case]
+    km_mod.REFRESH = refresh if rank == 0 else 1000   # rank 0's value wins
+    init = {}
+    orig = km_mod._init_centers
+
+    def rec(*args):
+        c = orig(*args)
+        init["c"] = np.array(c.toarray() if hasattr(c, "toarray") else c)
+        return c
+    km_mod._init_centers = rec
+    x = data(a.case)
+    ds = shard_dataset(load_data(x, sub))
+    km = KMeans(n_clusters=k, max_iter=iters, tol=tol, random_state=rs)
+    km.fit_predict(ds)
+    np.savez("%s.%d.npz" % (a.out, rank), centers=km.centers,
+             n_iter=km.n_iter, labels=ds.labels_int32(), init=init["c"],
+             refresh=np.array(km_mod.REFRESH))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

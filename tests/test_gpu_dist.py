@@ -1,0 +1,115 @@
+"""Multi-process / collective tests on the GPU.
+
+* The RCCL all-reduce behind the C ABI (``dkm_allreduce_*``): world size 1
+  through both set-up paths (one box = one GPU, and RCCL refuses two ranks
+  on one device).
+* The product Lloyd loop at world size 2: two processes on cuda:0 (gloo on
+  the CUDA buffers), each fitting its shard with the HIP kernels, against
+  the oracle on the whole dataset -- labels bit-exact, centres within 1e-9,
+  n_iter, the delta/refresh state kept consistent across ranks (rank 0's
+  DKM_REFRESH wins) and ``random_state=None`` (rank 0's draw is used).
+"""
+import ctypes
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import kmeans_oracle as orc
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def test_rccl_allreduce_world1_both_setups():
+    from dislib_amd import _lib
+    so = _lib.lib()
+    buf = torch.arange(1000, dtype=torch.float64, device="cuda") * 0.5
+    ref = buf.clone()
+    devs = (ctypes.c_int * 1)(0)
+    _lib.check(so.dkm_allreduce_init(1, devs), "init")
+    _lib.check(so.dkm_allreduce_sum_f64(ctypes.c_void_p(buf.data_ptr()),
+                                        buf.numel(), 0, _stream()), "sum")
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)
+    # a second communicator on the same device is refused
+    assert so.dkm_allreduce_init(1, devs) == 10001
+    _lib.check(so.dkm_allreduce_finalize(), "finalize")
+    uid = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
+    _lib.check(so.dkm_allreduce_unique_id(uid), "unique_id")
+    _lib.check(so.dkm_allreduce_init_rank(bytes(uid.raw), 1, 0, 0), "rank")
+    _lib.check(so.dkm_allreduce_sum_f64(ctypes.c_void_p(buf.data_ptr()),
+                                        buf.numel(), 0, _stream()), "sum")
+    torch.cuda.synchronize()
+    assert torch.equal(buf, ref)
+    assert so.dkm_allreduce_sum_f64(None, 5, 0, _stream()) == 10001
+    _lib.check(so.dkm_allreduce_finalize(), "finalize")
+    assert so.dkm_allreduce_sum_f64(ctypes.c_void_p(buf.data_ptr()), 5, 0,
+                                    _stream()) == 10001   # no communicator
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run_world2(case, tmp_path):
+    out = str(tmp_path / case)
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case,
+           "--out", out]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return [dict(np.load("%s.%d.npz" % (out, i))) for i in range(2)]
+
+
+@pytest.mark.parametrize("case", ["dense", "gemm", "none", "ragged"])
+def test_world2_fit_predict_vs_oracle(case, tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import dist_worker as w
+    n, d, blobs, k, sub, iters, tol, rs, refresh = w.CASES[case]
+    r0, r1 = _run_world2(case, tmp_path)
+    # replicated state: identical bits on both ranks
+    assert np.array_equal(r0["centers"], r1["centers"])
+    assert int(r0["n_iter"]) == int(r1["n_iter"])
+    if rs is not None:   # with None each rank draws; rank 0's draw is used
+        assert np.array_equal(r0["init"], r1["init"])
+    # the oracle on the whole dataset from the same initial centres
+    x = w.data(case)
+    blocks = [x[i:i + sub] for i in range(0, n, sub)]
+    ref = orc.OracleKMeans(n_clusters=k, max_iter=iters, tol=tol,
+                           random_state=0)
+    real_init = orc.init_centers
+    orc.init_centers = lambda *a: r0["init"].copy()
+    try:
+        rl = ref.fit(blocks, set_labels=True)
+    finally:
+        orc.init_centers = real_init
+    assert int(r0["n_iter"]) == ref.n_iter
+    lab = np.concatenate([r0["labels"], r1["labels"]])
+    assert np.array_equal(lab, rl)
+    err = np.max(np.abs(r0["centers"] - ref.centers) /
+                 np.maximum(np.abs(ref.centers), 1.0))
+    assert err <= 1e-9, err

@@ -574,3 +574,45 @@ def test_f16_c1_full_size(mode):
     assert km.n_iter == int(g["n_iter"])
     assert np.array_equal(ds.labels_int32(), g["labels"].astype(np.int32))
     _close(km.centers, g["centers"], RTOL64)
+
+
+def test_subset_reassignment_refreshes_device_image():
+    """The HBM image follows the Subsets: re-assigning a Subset's samples
+    (or concatenating) between two fits gives the result of a fresh
+    Dataset, not of the stale upload (DeviceData cache)."""
+    rng = np.random.default_rng(31)
+    x1 = rng.standard_normal((3000, 12)) * 3
+    x2 = x1.copy()
+    x2[:1000] += 7.0
+    ds = _load(x1, 1000)
+    km = _km(n_clusters=4, max_iter=3, tol=0, random_state=1)
+    km.fit_predict(ds)
+    ds[0].samples = x2[:1000].copy()          # reassignment
+    km.fit_predict(ds)
+    fresh = _load(x2, 1000)
+    km2 = _km(n_clusters=4, max_iter=3, tol=0, random_state=1)
+    km2.fit_predict(fresh)
+    assert np.array_equal(_labels(ds), _labels(fresh))
+    _close(km.centers, km2.centers, 1e-12)
+    ds[1].concatenate(ds[2])                  # 2000 rows in Subset 1
+    ref = orc.OracleKMeans(n_clusters=4, max_iter=3, tol=0, random_state=1)
+    rl = ref.fit([ds[0].samples, ds[1].samples, ds[2].samples],
+                 set_labels=True)
+    km.fit_predict(ds)
+    assert np.array_equal(_labels(ds), rl)
+
+
+def test_explicit_device_index():
+    """KMeans(device='cuda:0') with another current device would launch on
+    the wrong GPU without the device context; on one GPU this pins that
+    an explicit index works end to end."""
+    x = np.random.default_rng(2).standard_normal((2000, 8))
+    ds = _load(x, 500)
+    km = _km(n_clusters=3, max_iter=2, tol=0, random_state=0, device="cuda:0")
+    km.fit_predict(ds)
+    ref = orc.OracleKMeans(n_clusters=3, max_iter=2, tol=0, random_state=0)
+    rl = ref.fit([x[i:i + 500] for i in range(0, 2000, 500)], set_labels=True)
+    assert np.array_equal(_labels(ds), rl)
+    p = _load(x, 700)
+    km.predict(p)
+    assert np.array_equal(_labels(p), orc.predict_labels(x, km.centers))

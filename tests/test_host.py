@@ -171,3 +171,12 @@ def test_randomstate_instance_rejected():
     ds = load_data(np.random.random((10, 2)), subset_size=5)
     with pytest.raises(TypeError):
         KMeans(n_clusters=2, random_state=np.random.RandomState(0)).fit(ds)
+
+
+def test_device_must_be_a_gpu():
+    """KMeans(device=...) names the GPU that runs the kernels; anything
+    that is not a ROCm device is rejected before any launch."""
+    pytest.importorskip("torch")
+    from dislib_amd import _device
+    with pytest.raises(ValueError, match="ROCm GPU"):
+        _device.resolve("cpu")

@@ -243,6 +243,26 @@ def test_txt_column_mismatch_raises(tmp_path):
         load_txt_file(str(p), 10, 3)
 
 
+@pytest.mark.parametrize("ending", ["\n", "\r\n", "\r"])
+def test_txt_width_changes_between_chunks(tmp_path, ending):
+    """genfromtxt runs per chunk in the reference: a file whose width
+    changes at a chunk boundary loads (one width per Subset); a change
+    inside a chunk raises ValueError in both."""
+    rng = np.random.default_rng(12)
+    a = _csv_text(rng, 30, 3, extras=False).splitlines()
+    b = _csv_text(rng, 20, 5, extras=False).splitlines()
+    p = tmp_path / "r.csv"
+    p.write_bytes((ending.join(a + b) + ending).encode())
+    ds = load_txt_file(str(p), 10, 5)
+    ref = orc.load_file(str(p), 10, "txt", 5, delimiter=",")
+    _check(ds, ref, False)
+    assert [s.samples.shape[1] for s in ds] == [3, 3, 3, 5, 5]
+    with pytest.raises(ValueError):
+        orc.load_file(str(p), 25, "txt", 5, delimiter=",")
+    with pytest.raises(ValueError):
+        load_txt_file(str(p), 25, 5)
+
+
 def test_txt_files(tmp_path):
     rng = np.random.default_rng(9)
     d = tmp_path / "csvdir"

@@ -18,7 +18,7 @@ step() {  # name limit cmd...
 }
 step pytest 600 python -u -m pytest tests -m gpu -v -p no:cacheprovider --maxfail=10 --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-DKM_VERBOSE=1 step verbose 120 python bench.py --steps 2 --warmup 1 --no-cpu
+# (resident-block sizing: build a -DDKM_AB_VERBOSE variant with variants.sh)
 if [ $# -gt 0 ]; then
   bash tools/ab_libs.sh $TAG main "$@" || exit $?
 fi
