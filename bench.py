@@ -76,16 +76,17 @@ def cpu_share():
     return max(1, min(share, aff)), aff
 
 
-def cpu_baseline(d, k, target_s, centers, n_blobs):
+def cpu_baseline(d, k, target_s, centers, n_blobs, share):
     """One Lloyd iteration's partial sums on a bounded sample of the same
-    workload, one Subset per task over a process pool (BLAS threads 1),
-    then the arity-50 merge and the centre update -- the reference's task
-    graph (base.py:113-147) run by the vectorised oracle."""
-    os.environ["OMP_NUM_THREADS"] = "1"
+    workload, one Subset per task over a process pool of `share` = (cores,
+    machine threads) workers (BLAS threads 1), then the arity-50 merge and
+    the centre update -- the reference's task graph (base.py:113-147) run
+    by the vectorised oracle."""
+    cores, machine = share
+    os.environ["OMP_NUM_THREADS"] = "1"        # BLAS threads of the workers
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
     import multiprocessing as mp
     from oracle import kmeans_oracle as orc
-    cores, machine = cpu_share()
     # probe: single-core rate on a small block (smaller for large k*d)
     probe = int(max(16, min(4000, 3e8 / (k * d))))
     xb, _ = orc.make_blobs_rows(0, probe, d, n_blobs, seed=0)
@@ -246,11 +247,12 @@ def main():
     cpu = {}
     if world == 1 and not a.no_cpu:
         from dislib_amd.cluster.kmeans import _init_centers as _ic
+        share = cpu_share()       # before the workers' BLAS settings below
         cpu["head"] = cpu_baseline(a.d, a.k, a.cpu_seconds,
-                                   _ic(a.d, False, a.k, 0), a.k)
+                                   _ic(a.d, False, a.k, 0), a.k, share)
         for i, (_, n, d, k, *_r) in enumerate(extras):
             cpu[i] = cpu_baseline(d, k, a.cpu_seconds / 2,
-                                  _ic(d, False, k, 0), k)
+                                  _ic(d, False, k, 0), k, share)
 
     import torch
     import torch.distributed as dist
