@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get("DKM_LIB", os.path.join(_HERE, "libdkm.so"))
 
 # constants mirrored from include/dkm.h
 ABI_VERSION = 1
-MODE_AUTO, MODE_EXACT, MODE_SCREEN32, MODE_BF16X3 = 0, 1, 2, 3
+MODE_AUTO, MODE_EXACT, MODE_SCREEN32, MODE_BF16X3, MODE_BF16 = 0, 1, 2, 3, 4
 SUMS_F64, SUMS_F32, SUMS_RECIP = 0, 1, 2
 PREP_CSR = 1
 COMM_ID_BYTES = 128

@@ -23,8 +23,8 @@ accumulated in a different order than the reference's sequential
 Subset-then-arity-tree order, so centres agree to ~1e-15 relative instead of
 bit-for-bit; ``arity`` is kept but has no effect on the GPU (no reduction
 tree).  Extra keyword-only arguments select the assignment arithmetic
-(``mode``: "auto" | "exact" | "screen32" | "bf16x3", identical labels) and
-the device.
+(``mode``: "auto" | "exact" | "screen32" | "bf16x3" | "bf16", identical
+labels) and the device.
 """
 import os
 
@@ -34,7 +34,8 @@ from scipy.sparse import csr_matrix, issparse
 from .. import _lib, _shard
 
 _MODES = {"auto": _lib.MODE_AUTO, "exact": _lib.MODE_EXACT,
-          "screen32": _lib.MODE_SCREEN32, "bf16x3": _lib.MODE_BF16X3}
+          "screen32": _lib.MODE_SCREEN32, "bf16x3": _lib.MODE_BF16X3,
+          "bf16": _lib.MODE_BF16}
 
 
 def _init_centers(n_features, sparse, n_clusters, random_state):
@@ -214,13 +215,19 @@ class _Lloyd:
         from .._device import assign_delta, partial_sum
         if self.dd.n == 0:
             return
+        # "auto": the first iteration scores against the initial centres,
+        # where the single-product screen the library picks for large k x d
+        # would leave most samples undecided -- screen it with bf16x3
+        mode = self.mode
+        if mode == _lib.MODE_AUTO and self.it == 0:
+            mode = _lib.MODE_BF16X3
         with self._on():
             if self._full():
                 partial_sum(self.dd, self.C, self.ws, self.labels, self.acc,
-                            self.mode)
+                            mode)
             else:
                 assign_delta(self.dd, self.C, self.ws, self.labels, self.acc,
-                             self.mode)
+                             mode)
 
     def assign(self):
         self.prepare()

@@ -334,7 +334,7 @@ __global__ void __launch_bounds__(BLOCK)
 // `packed` adds that to B (both compared scores move, and the test is
 // s2 - s1 > 2B).
 // ---------------------------------------------------------------------------
-enum { P_F32 = 0, P_B3 = 1 };
+enum { P_F32 = 0, P_B3 = 1, P_B1 = 2 };
 
 constexpr uint32_t PACK_BITS = 7;
 constexpr uint32_t PACK_MASK = (1u << PACK_BITS) - 1;
@@ -1319,6 +1319,308 @@ __global__ void __launch_bounds__(SBW) __attribute__((
   }
 }
 
+// ---------------------------------------------------------------------------
+// Single-product screen (P_B1) for k x d beyond the LDS sums budget with the
+// bf16 centres resident in LDS (b1_ok: C3's k = 1000, d = 64).  One product
+// per term -- xh.ch on v_mfma_f32_32x32x16_bf16 -- a third of bf16x3's
+// matrix work, with its own bound:
+//   x -> fl32 -> bf16 and -2c -> fl32 -> bf16 (round to nearest) lose
+//   <= 2^-9 each: 1.02 * 2^-8 sum|x (-2c)|; the fp32 chain of dpad products
+//   + |c|^2 (dpad + 2) 2^-23; packing 2^PACK1 ulp; numpy's rounding; all as
+//   screen_bound's terms, B doubled for safety.
+// The looser bound leaves ~5% of converged C3 samples undecided, nearly all
+// with exactly two candidates, so each lane keeps a packed top-3 (4 VALU
+// ops per score: pack, 2 x med3, min) and the decision is three-way:
+//   s2 - s1 > 2B            -> the label;
+//   s3 - s1 > 2B (else)     -> candidates {c1, c2}: the per-wave candidate
+//                              list (k_cand2: reference arithmetic on both);
+//   otherwise               -> the re-check list (k_recheck_list).
+// Labels only (amode none): the sums of these shapes come from
+// k_label_sums.  Lane l = (r = l & 31, h = l >> 5) holds features
+// 16ks + 8h .. +7 of sample r for every K-step ks; accumulator register g
+// = centre cb*32 + (g & 3) + 8 (g >> 2) + 4h, tag = (block in group) x 16 + g
+// in PACK1 = 9 bits (groups of 32 blocks = 1024 centres).
+// ---------------------------------------------------------------------------
+// 16 waves per CU (one block: the centres fill the LDS), <= 128 VGPRs: no
+// register prefetch of the next tile -- the CU's other waves cover a
+// wave's load (at 2 waves per SIMD with a prefetched tile the kernel waited
+// 48% of its cycles: PMC r02a)
+constexpr int SBB = 1024;
+constexpr uint32_t PACK1 = 9, PACK1_MASK = (1u << PACK1) - 1;
+template <class TX, int NKS>
+__global__ void __launch_bounds__(SBB)
+    k_screen_b1(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
+                int k, WsView v, int32_t *__restrict__ lab_out, int64_t base,
+                int delta) {
+  constexpr int GB = 1 << (PACK1 - 4);  // 32-centre blocks per group
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nkb = (int)(kpad32(k) / 32);
+  char *frag = (char *)smem;                                // nkb x NKS KB
+  float *cn = (float *)(frag + (int64_t)nkb * NKS * 1024);  // nkb x 32
+  {
+    const f32x4 *src = (const f32x4 *)v.b1frag;
+    f32x4 *dst = (f32x4 *)frag;
+    for (int e = threadIdx.x; e < nkb * NKS * 64; e += SBB) dst[e] = src[e];
+    for (int e = threadIdx.x; e < nkb * 32; e += SBB) cn[e] = v.cn32f[e];
+  }
+  const float cm =
+      (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
+  // bound constants (screen_bound's terms with the single-product split)
+  const float rel = 1.02f * 0x1.0p-8f + (16.0f * NKS + 2.0f) * 0x1.0p-23f;
+  BoundK bk = bound_consts<P_F32>(d, cm);
+  bk.k_mag = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(
+      2.0f * (2.0f * rel + 0x1.0p-23f * (float)(1u << PACK1)) * 1.0001f)));
+  const float ninf = __uint_as_float(opaque_u32(0xff800000u));
+  const uint32_t vmask = opaque_u32(~PACK1_MASK);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t wv = (int64_t)blockIdx.x * (SBB / 64) + wid;
+  const int64_t step = (int64_t)gridDim.x * (SBB / 64) * 32;
+  int2 *wl = v.tlist + wv * TL_CAP;  // >= 3 candidates
+  int2 *cl = v.clist + wv * B1_CAP;  // 2 candidates
+  const bool listing = wv < TL_SEGS && wv < B1_SEGS;
+  int tl_cnt = 0, cl_cnt = 0, tl_over = 0;
+
+  double tile[NKS][8];
+  int pv = -1;
+  const uint32_t lane_off = (uint32_t)(r * ldx * (int64_t)sizeof(TX)) +
+                            (uint32_t)(8 * h * sizeof(TX));
+  auto load_tile = [&](int64_t s0) {
+    const int64_t rows = std::max<int64_t>(0, n - s0);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(X + std::min(s0, n) * ldx), 0,
+        (int)std::min<int64_t>(rows * ldx * (int64_t)sizeof(TX), 0x7fffffff),
+        0x00020000);
+    if (delta) {
+      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(lab_out + std::min(s0, n)), 0,
+          (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
+      pv = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
+    }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (16 * ks + 8 * h < d) {
+        const int o = 16 * ks * (int)sizeof(TX);
+        if constexpr (sizeof(TX) == 8) {
+#pragma unroll
+          for (int p4 = 0; p4 < 4; ++p4) {
+            const double2 v2 = __builtin_bit_cast(
+                double2, __builtin_amdgcn_raw_buffer_load_b128(
+                             rx, lane_off, o + 16 * p4, 0));
+            tile[ks][2 * p4] = v2.x;
+            tile[ks][2 * p4 + 1] = v2.y;
+          }
+        } else {
+#pragma unroll
+          for (int p4 = 0; p4 < 2; ++p4) {
+            const float4 v4 = __builtin_bit_cast(
+                float4, __builtin_amdgcn_raw_buffer_load_b128(
+                            rx, lane_off, o + 16 * p4, 0));
+            tile[ks][4 * p4] = v4.x;
+            tile[ks][4 * p4 + 1] = v4.y;
+            tile[ks][4 * p4 + 2] = v4.z;
+            tile[ks][4 * p4 + 3] = v4.w;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) tile[ks][m] = 0.0;
+      }
+    }
+  };
+
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  for (int64_t s0 = base + wv * 32; s0 < n; s0 += step) {
+    load_tile(s0);
+    float xx = 0.f;
+    bf16x8 xh[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int m = 0; m < 8; m += 2) {
+        const float x0 = (float)tile[ks][m];
+        const float x1 = (float)tile[ks][m + 1];
+        xx = fmaf(x0, x0, xx);
+        xx = fmaf(x1, x1, xx);
+        const bf16x2 h2 = __builtin_convertvector(f32x2{x0, x1}, bf16x2);
+        xh[ks][m] = h2[0];
+        xh[ks][m + 1] = h2[1];
+      }
+    {
+      float xa, xb;
+      pair_xor<32>(xx, xa, xb);
+      xx = xa + xb;
+    }
+    const int prv = pv;
+
+    // running (value, centre) top-3 of this lane over all groups
+    float r1 = INFINITY, r2 = INFINITY, r3 = INFINITY;
+    int i1 = 0, i2 = 0, i3 = 0;
+    auto chain = [&](int cb, f32x16 &accv) {
+      const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
+      const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
+      accv = f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                    c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8 ah =
+            *(const bf16x8 *)(frag + ((int64_t)cb * NKS + ks) * 1024 +
+                              lane * 16);
+        accv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xh[ks], accv, 0, 0,
+                                                       0);
+      }
+    };
+    for (int g0 = 0; g0 < nkb; g0 += GB) {
+      const int g1 = min(nkb, g0 + GB);
+      // two independent packed top-3 chains (even / odd registers): half
+      // the dependency depth of one chain; merged at the group fold
+      float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
+      float e1 = INFINITY, e2 = INFINITY, e3 = INFINITY;
+      auto score = [&](int cb, const f32x16 &accv) {
+        const uint32_t t0 = opaque_s32((uint32_t)((cb - g0) * 16));
+#pragma unroll
+        for (int g = 0; g < 16; g += 2) {
+          const float sp =
+              __uint_as_float((__float_as_uint(accv[g]) & vmask) | (t0 + g));
+          const float sq = __uint_as_float(
+              (__float_as_uint(accv[g + 1]) & vmask) | (t0 + g + 1));
+          b3 = __builtin_amdgcn_fmed3f(b2, b3, sp);
+          b2 = __builtin_amdgcn_fmed3f(b1, b2, sp);
+          b1 = min_nc(b1, sp, ninf);
+          e3 = __builtin_amdgcn_fmed3f(e2, e3, sq);
+          e2 = __builtin_amdgcn_fmed3f(e1, e2, sq);
+          e1 = min_nc(e1, sq, ninf);
+        }
+      };
+      f32x16 acc_a, acc_b;
+      chain(g0, acc_a);
+      int cb = g0;
+      for (; cb + 2 <= g1; cb += 2) {  // ping-pong: no runtime-indexed arrays
+        chain(cb + 1, acc_b);
+        score(cb, acc_a);
+        if (cb + 2 < g1) chain(cb + 2, acc_a);
+        score(cb + 1, acc_b);
+      }
+      if (cb < g1) score(cb, acc_a);
+      // fold the group's packed top-3 into the running (value, index) top-3
+      auto gidx = [&](float p) {
+        const uint32_t tg = __float_as_uint(p) & PACK1_MASK;
+        const int g = (int)(tg & 15);
+        return (g0 + (int)(tg >> 4)) * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+      };
+      auto ins = [&](float p) {
+        const int pi = gidx(p);
+        const bool c1 = p < r1, c2 = p < r2, c3 = p < r3;
+        r3 = c2 ? r2 : (c3 ? p : r3);
+        i3 = c2 ? i2 : (c3 ? pi : i3);
+        r2 = c1 ? r1 : (c2 ? p : r2);
+        i2 = c1 ? i1 : (c2 ? pi : i2);
+        r1 = c1 ? p : r1;
+        i1 = c1 ? pi : i1;
+      };
+      ins(b1);
+      ins(b2);
+      ins(b3);
+      ins(e1);
+      ins(e2);
+      ins(e3);
+    }
+    {  // merge the two lanes of a sample: the top-3 of both triples under
+       // the (value, index) order, so both lanes build the same triple
+      const float o1 = __shfl_xor(r1, 32, 64), o2 = __shfl_xor(r2, 32, 64),
+                  o3 = __shfl_xor(r3, 32, 64);
+      const int j1 = __shfl_xor(i1, 32, 64), j2 = __shfl_xor(i2, 32, 64),
+                j3 = __shfl_xor(i3, 32, 64);
+      auto lt = [](float a, int ia, float b, int ib) {
+        return a < b || (a == b && ia < ib);
+      };
+      auto ins3 = [&](float p, int pi) {
+        const bool c1 = lt(p, pi, r1, i1), c2 = lt(p, pi, r2, i2),
+                   c3 = lt(p, pi, r3, i3);
+        r3 = c2 ? r2 : (c3 ? p : r3);
+        i3 = c2 ? i2 : (c3 ? pi : i3);
+        r2 = c1 ? r1 : (c2 ? p : r2);
+        i2 = c1 ? i1 : (c2 ? pi : i2);
+        r1 = c1 ? p : r1;
+        i1 = c1 ? pi : i1;
+      };
+      ins3(o1, j1);
+      ins3(o2, j2);
+      ins3(o3, j3);
+    }
+    const int64_t si = s0 + r;
+    float xn;
+    const float B2 = bound2_fast(bk, xx, xn);
+    const bool sane = (xn < 1e18f) & (xn * cm < 1e30f) & (r1 < 1e30f);
+    const bool unique = sane & (r2 - r1 > B2);
+    const bool two = sane & !unique & (r3 - r1 > B2);
+    const bool valid = si < n && h == 0;
+    const int prev = delta ? prv : -1;
+    // two candidates -> candidate list, more -> re-check list
+    const uint64_t mc = __ballot(valid && two);
+    const uint64_t mt = __ballot(valid && !unique && !two);
+    const int addc = __popcll(mc), addt = __popcll(mt);
+    bool spill = false;  // list full: the label scan finds the sample
+    if (listing && cl_cnt + addc <= B1_CAP) {
+      if (valid && two)
+        cl[cl_cnt + lane_prefix(mc)] =
+            make_int2((int)(si - base), i1 | (i2 << 16));
+      cl_cnt += addc;
+    } else {
+      spill = valid && two;
+      tl_over += addc;
+    }
+    if (listing && tl_cnt + addt <= TL_CAP) {
+      if (valid && !unique && !two)
+        wl[tl_cnt + lane_prefix(mt)] = make_int2((int)(si - base), prev);
+      tl_cnt += addt;
+    } else {
+      spill |= valid && !unique && !two;
+      tl_over += addt;
+    }
+    (void)spill;
+    if (valid && !(unique && i1 == prev))
+      lab_out[si] = unique ? i1 : -(prev + 2);
+  }
+  if (lane == 0 && listing) {
+    v.tcount[wv] = tl_cnt;
+    v.ccount[wv] = cl_cnt;
+  }
+  if (lane == 0 && tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
+}
+
+// Two-candidate samples of k_screen_b1: lane per entry, the reference
+// arithmetic (numpy pairwise order, correctly rounded sqrt) on c1 and c2,
+// first index among equal distances.  Labels only.
+template <class TX>
+__global__ void __launch_bounds__(BLOCK)
+    k_cand2(const TX *__restrict__ X, int d, int64_t ldx,
+            const double *__restrict__ C, WsView v,
+            int32_t *__restrict__ lab_out, int64_t base, int nseg) {
+  const int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+  const int64_t nwv = (int64_t)gridDim.x * (BLOCK / 64);
+  const int lane = threadIdx.x & 63;
+  unsigned long long mine = 0;
+  // (segment, 64-entry batch) pairs over all waves, batch index major
+  for (int64_t L = wv; L < (int64_t)nseg * (B1_CAP / 64); L += nwv) {
+    const int64_t sg = L % nseg;
+    const int t0 = (int)(L / nseg) * 64;
+    const int cnt = v.ccount[sg];
+    if (t0 == 0 && lane == 0) mine += cnt;
+    if (t0 + lane >= cnt) continue;
+    const int2 it = v.clist[sg * B1_CAP + t0 + lane];
+    const int64_t si = base + it.x;
+    const int c1 = it.y & 0xffff, c2 = (int)((unsigned)it.y >> 16);
+    const TX *xr = X + si * ldx;
+    const double d1 = sqrt(pw_sum(SqDiff<TX>{xr, C + (int64_t)c1 * d}, d));
+    const double d2 = sqrt(pw_sum(SqDiff<TX>{xr, C + (int64_t)c2 * d}, d));
+    lab_out[si] = (d2 < d1 || (d2 == d1 && c2 < c1)) ? c2 : c1;
+  }
+  if (mine) atomicAdd((unsigned long long *)&v.hdr->rechecked_total, mine);
+}
+
 // Exact re-check of the samples the screen left undecided (lab_out < 0,
 // encoding the previous label as -(prev + 2)).  Waves scan 64 labels at a
 // time (coalesced, no shared counter).
@@ -1938,13 +2240,75 @@ static int launch_label_sums(const TX *X, int64_t lo, int64_t hi, int d,
   return check_launch("label sums");
 }
 
+// Do the [sums | counts] of k x d fit block-private LDS beside the screen's
+// fragments (else the screens write labels and k_label_sums sums)?
+static bool sums_fit_lds(int64_t k, int64_t d) {
+  const size_t a = (size_t)lds_acc_len(k, (int)d) * 8;
+  const size_t f = d <= 32 ? (size_t)(kpad32(k) / 32) * (4096 + 128)
+                           : screen_lds_fixed(k, d);
+  return f + a <= LDS_BUDGET;
+}
+
+template <class TX>
+static int launch_screen_b1(const TX *X, int64_t end, int d, int64_t ldx,
+                            int k, const WsView &v, int32_t *lab_out,
+                            int64_t base, hipStream_t s, int *nseg) {
+  const size_t lds = b1_frag_bytes(k, d);
+  const int nks = (int)(dpad16(d) / 16);
+  const void *kf = nullptr;
+#define DKM_B1(N)                                            \
+  case N:                                                    \
+    kf = (const void *)k_screen_b1<TX, N>;                   \
+    break;
+  switch (nks) {
+    DKM_B1(1) DKM_B1(2) DKM_B1(3) DKM_B1(4)
+    DKM_B1(5) DKM_B1(6) DKM_B1(7) DKM_B1(8)
+    default:
+      return fail(DKM_E_ARG, "screen_b1: d too large");
+  }
+#undef DKM_B1
+  if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "screen_b1: LDS attribute");
+  const int64_t need = (end - base + 32 * (SBB / 64) - 1) / (32 * (SBB / 64));
+  const unsigned g = (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>(need, (int64_t)dev_info().cus));
+  *nseg = (int)std::min<int64_t>((int64_t)g * (SBB / 64),
+                                 std::min(TL_SEGS, B1_SEGS));
+  const int delta = 0;  // labels only (amode none): no previous label
+  switch (nks) {
+#define DKM_B1L(N)                                                          \
+  case N:                                                                   \
+    k_screen_b1<TX, N><<<g, SBB, lds, s>>>(X, end, d, ldx, k, v, lab_out,   \
+                                           base, delta);                    \
+    break;
+    DKM_B1L(1) DKM_B1L(2) DKM_B1L(3) DKM_B1L(4)
+    DKM_B1L(5) DKM_B1L(6) DKM_B1L(7) DKM_B1L(8)
+#undef DKM_B1L
+  }
+  return check_launch("screen assignment (single product)");
+}
+
+template <class TX>
+static int launch_cand2(const TX *X, int d, int64_t ldx, const double *C,
+                        const WsView &v, int32_t *lab_out, int64_t base,
+                        int nseg, hipStream_t s) {
+  const int64_t units = (int64_t)nseg * (B1_CAP / 64);
+  const int64_t g = std::max<int64_t>(
+      1, std::min<int64_t>((int64_t)dev_info().cus * 8,
+                           (units + BLOCK / 64 - 1) / (BLOCK / 64)));
+  k_cand2<TX><<<(unsigned)g, BLOCK, 0, s>>>(X, d, ldx, C, v, lab_out, base,
+                                            nseg);
+  return check_launch("two-candidate re-check");
+}
+
 // Screen + exact re-check over [0, n).  Labels go to `labels` when given,
 // else to the workspace scratch (queue region), in chunks of its capacity.
 template <class TX>
 static int launch_screen(int prec, const TX *X, int64_t n, int d,
-                         int64_t ldx, int k, const WsView &v, size_t wsb,
-                         int32_t *labels, double *acc, int acc_kind,
-                         hipStream_t s) {
+                         int64_t ldx, const double *C, int k, const WsView &v,
+                         size_t wsb, int32_t *labels, double *acc,
+                         int acc_kind, hipStream_t s) {
   const size_t fixed = (size_t)((const char *)v.queue - (const char *)v.hdr);
   const int64_t nq =
       std::min<int64_t>((int64_t)((wsb - fixed) / 4), INT32_MAX);
@@ -1953,6 +2317,12 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const int64_t chunk = labels ? n : nq;
   const bool vec = (d % 8 == 0) && (ldx % (16 / (int64_t)sizeof(TX)) == 0) &&
                    (((uintptr_t)X % 16) == 0);
+  // single-product screen: labels only, so the sums must come from
+  // k_label_sums (full sums, or delta against a copy of the old labels)
+  const bool b1 = prec == P_B1 && v.b1frag && vec &&
+                  (int64_t)32 * ldx * (int64_t)sizeof(TX) < (1ll << 31) &&
+                  (acc_kind == 0 || acc_kind == 1 || (labels && nq >= n));
+  if (prec == P_B1 && !b1) prec = P_B3;
   // d <= 32 bf16x3 with the 32x32x16 fragments resident: k_screen_w32
   const size_t fb32 = (size_t)(kpad32(k) / 32) * (4096 + 128);
   const bool w32 = prec == P_B3 && d <= 32 && vec && fb32 <= LDS_BUDGET &&
@@ -1970,7 +2340,7 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   // AB_DELTA_POST: delta sums from k_label_sums even when they fit LDS
   // (the screen then needs only the fragments' LDS: more blocks per CU)
   const bool force_post = acc_kind == 2 && AB_DELTA_POST;
-  const bool post = acc_kind != 0 && (!lds_fits || force_post) &&
+  const bool post = acc_kind != 0 && (!lds_fits || force_post || b1) &&
                     !AB_NO_POST &&
                     (acc_kind == 1 || (labels && nq >= n));
   const int32_t *prevbuf = nullptr;
@@ -1988,7 +2358,12 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
     const int64_t end = std::min(n, base + chunk);
     int32_t *lab_out = labels ? labels : v.queue - base;
     int r, nseg = 0;
-    if (w32)
+    if (b1) {
+      if ((r = launch_screen_b1<TX>(X, end, d, ldx, k, v, lab_out, base, s,
+                                    &nseg)))
+        return r;
+      r = launch_cand2<TX>(X, d, ldx, C, v, lab_out, base, nseg, s);
+    } else if (w32)
       r = launch_screen_w32<TX>(X, end, d, ldx, k, v, lab_out, acc, amode,
                                 base, lds, use_list, s, &nseg);
     else if (prec == P_F32)
@@ -2006,8 +2381,9 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                                                    lab_out, acc, amode, base,
                                                    lds, use_list, chb, s, &nseg);
     if (r) return r;
-    if (use_list && (r = launch_list<TX>(X, d, ldx, k, v, lab_out, acc,
-                                         skind, vec, base, nseg, s)))
+    if ((use_list || b1) && (r = launch_list<TX>(X, d, ldx, k, v, lab_out,
+                                                  acc, skind, vec, base,
+                                                  nseg, s)))
       return r;
     if ((r = launch_recheck<TX>(X, end, d, ldx, k, v, lab_out, acc,
                                 skind, vec, base, s)))
@@ -2073,8 +2449,11 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
     return fail(DKM_E_ARG, std::string(who) + ": nothing to write");
   hipStream_t s = (hipStream_t)stream;
   if (mode == DKM_MODE_AUTO)
-    mode = screen_ok(k, d) || gemm_path(k, d) ? DKM_MODE_SCREEN_BF16X3
-                                              : DKM_MODE_EXACT;
+    mode = !screen_ok(k, d) && !gemm_path(k, d) ? DKM_MODE_EXACT
+           // sums beyond LDS and bf16 centres resident: the single product
+           : screen_ok(k, d) && b1_ok(k, d) && !sums_fit_lds(k, d)
+               ? DKM_MODE_SCREEN_BF16
+               : DKM_MODE_SCREEN_BF16X3;
   if (mode == DKM_MODE_EXACT)
     return launch_exact<TX>(X, n, (int)d, ldx, C, (int)k, labels, acc,
                             acc_kind, s);
@@ -2084,15 +2463,20 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
     return launch_gemm<TX>(X, n, (int)d, ldx, C, (int)k, v, wsb, labels, acc,
                            acc_kind, s);
   }
-  if (mode == DKM_MODE_SCREEN32 || mode == DKM_MODE_SCREEN_BF16X3) {
+  if (mode == DKM_MODE_SCREEN_BF16 && gemm_path(k, d))
+    mode = DKM_MODE_SCREEN_BF16X3;  // the GEMM screen's own precision
+  if (mode == DKM_MODE_SCREEN32 || mode == DKM_MODE_SCREEN_BF16X3 ||
+      mode == DKM_MODE_SCREEN_BF16) {
     if (!screen_ok(k, d))
       return launch_exact<TX>(X, n, (int)d, ldx, C, (int)k, labels, acc,
                               acc_kind, s);
     WsView v;
     if (int r = ws_view(ws, wsb, k, d, &v)) return r;
-    return launch_screen<TX>(mode == DKM_MODE_SCREEN32 ? P_F32 : P_B3, X, n,
-                             (int)d, ldx, (int)k, v, wsb, labels, acc,
-                             acc_kind, s);
+    const int prec = mode == DKM_MODE_SCREEN32 ? P_F32
+                     : mode == DKM_MODE_SCREEN_BF16 ? P_B1
+                                                    : P_B3;
+    return launch_screen<TX>(prec, X, n, (int)d, ldx, C, (int)k, v, wsb,
+                             labels, acc, acc_kind, s);
   }
   return fail(DKM_E_ARG, std::string(who) + ": bad mode");
 }

@@ -54,6 +54,26 @@ constexpr int GTOP = 4;                 // (score, centre) pairs kept per sample
 
 __host__ __device__ inline int64_t kpad256(int64_t k) { return (k + 255) / 256 * 256; }
 
+// ---------------------------------------------------------------------------
+// Single-product screen (k_screen_b1, dkm_dense.hip): bf16 hi of x and -2c
+// on v_mfma_f32_32x32x16_bf16, every centre resident in LDS (32-centre
+// blocks x 16-feature K-steps, 1 KB each), a packed top-3 per sample; two
+// candidates within the bound go to a per-wave candidate list (B1_CAP
+// entries of (offset, c1 | c2 << 16)), three or more to the re-check lists.
+// ---------------------------------------------------------------------------
+constexpr int B1_SEGS = 4096;          // >= 256 CUs x 8 waves
+constexpr int B1_CAP = 4096;           // candidate entries per screen wave
+constexpr size_t B1_LDS_MAX = 150 * 1024;
+
+__host__ __device__ inline int64_t dpad16(int64_t d);
+inline size_t b1_frag_bytes(int64_t k, int64_t d) {
+  return (size_t)(((k + 31) / 32 * 32) * ((d + 15) / 16 * 16) * 2 +
+                  ((k + 31) / 32 * 32) * 4);
+}
+inline bool b1_ok(int64_t k, int64_t d) {
+  return d <= 128 && k >= 2 && k <= 32767 && b1_frag_bytes(k, d) <= B1_LDS_MAX;
+}
+
 // GEMM screen eligibility: the register-tile screen takes d <= 128
 inline bool gemm_path(int64_t k, int64_t d) {
   return d > 128 && k >= 2 && k <= 32767;
@@ -77,7 +97,11 @@ struct WsView {
   float *cnpad;   // kpad16 fp32 ||c||^2, 2^100 for padding centres
   uint16_t *bfrag; // bf16 hi/lo of -2*centres, 16x16x32 fragment order
   uint16_t *b32frag; // d <= 32: bf16 hi/lo, 32x32x16 order (k_screen_w32)
-  float *cn32f;   // d <= 32: kpad32 ||c||^2 in 32x32 accumulator order
+  float *cn32f;   // kpad32 ||c||^2 in 32x32 accumulator order
+  uint16_t *b1frag; // b1_ok: bf16 hi of -2c, 32x32x16 order, dpad16 / 16
+                    // K-steps per 32-centre block (k_screen_b1)
+  int2 *clist;     // b1_ok: B1_SEGS x B1_CAP (offset, c1 | c2 << 16)
+  int32_t *ccount; // b1_ok: entries used per screen wave
   int2 *tlist;    // TL_SEGS x TL_CAP undecided (offset, prev) per screen wave
   int32_t *tcount; // TL_SEGS entries used per screen wave
   // GEMM screen (gemm_path only; else NULL)

@@ -62,6 +62,11 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
   b += (size_t)TL_SEGS * TL_CAP * 8;  // tlist
   b += (size_t)TL_SEGS * 4;           // tcount
   b += gemm_bytes(k, d);
+  if (b1_ok(k, d)) {
+    b += round_up(kpad32(k) * dpad16(d) * 2, 256);  // b1frag
+    b += (size_t)B1_SEGS * B1_CAP * 8;              // clist
+    b += (size_t)B1_SEGS * 4;                       // ccount
+  }
   b += round_up(n_queue * 4, 256);    // queue
   return b;
 }
@@ -100,6 +105,9 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   v->gxn = nullptr;
   v->gpart = nullptr;
   v->gchunk = 0;
+  v->b1frag = nullptr;
+  v->clist = nullptr;
+  v->ccount = nullptr;
   if (gemm_path(k, d)) {
     const int64_t kp = kpad256(k), dp = dpad32(d), m = gemm_chunk(d);
     v->gchunk = m;
@@ -113,6 +121,14 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
     p += round_up(m * 4, 256);
     v->gpart = (int2 *)p;
     p += round_up(m * (kp / GT) * GTOP * 8, 256);
+  }
+  if (b1_ok(k, d)) {
+    v->b1frag = (uint16_t *)p;
+    p += round_up(kpad32(k) * dpad16(d) * 2, 256);
+    v->clist = (int2 *)p;
+    p += (size_t)B1_SEGS * B1_CAP * 8;
+    v->ccount = (int32_t *)p;
+    p += (size_t)B1_SEGS * 4;
   }
   v->queue = (int32_t *)p;
   const size_t fixed = (size_t)(p - (char *)ws);
@@ -198,11 +214,34 @@ __global__ void __launch_bounds__(256) k_frag(const double *__restrict__ C,
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < kp;
        c += (int64_t)gridDim.x * blockDim.x)
     v.cnpad[c] = c < k ? v.cn32[c] : 0x1.0p100f;
+  const int64_t nb32 = kpad32(k) / 32;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       e < nb32 * 32; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cb = e >> 5;
+    const int hh = (int)((e >> 4) & 1), g = (int)(e & 15);
+    const int64_t c = cb * 32 + (g & 3) + 8 * (g >> 2) + 4 * hh;
+    v.cn32f[e] = c < k ? v.cn32[c] : 0x1.0p100f;
+  }
+  if (v.b1frag) {
+    // k_screen_b1: block cb, K-step ks (16 features), lane l = (r, h),
+    // element j <- bf16(-2 c[cb*32 + r][16 ks + 8 h + j]); 1 KB per (cb, ks)
+    const int64_t nk16 = dpad16(d) / 16;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+         e < nb32 * nk16 * 512; e += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t blk = e >> 9;
+      const int w = (int)(e & 511), l = w >> 3, j = w & 7;
+      const int64_t cb = blk / nk16, ks = blk - cb * nk16;
+      const int64_t c = cb * 32 + (l & 31);
+      const int64_t t = 16 * ks + 8 * (l >> 5) + j;
+      const double x = (c < k && t < d) ? -2.0 * C[c * d + t] : 0.0;
+      v.b1frag[blk * 512 + l * 8 + j] =
+          __builtin_bit_cast(uint16_t, (__bf16)(float)x);
+    }
+  }
   if (d > 32) return;
   // 32x32x16 order (k_screen_w32): block cb, K-slice ks, lane l = (r, h),
   // element j <- -2 c[cb*32 + r][16h + 8ks + j]; |c|^2 of accumulator
   // register g of lane half h = centre cb*32 + (g & 3) + 8 (g >> 2) + 4h
-  const int64_t nb32 = kpad32(k) / 32;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
        e < nb32 * 1024; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t cb = e >> 10, w = e & 1023;
@@ -215,13 +254,6 @@ __global__ void __launch_bounds__(256) k_frag(const double *__restrict__ C,
     uint16_t *dst = v.b32frag + (cb * 2 + ks) * 1024;
     dst[l * 8 + j] = __builtin_bit_cast(uint16_t, hi);
     dst[512 + l * 8 + j] = __builtin_bit_cast(uint16_t, lo);
-  }
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-       e < nb32 * 32; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t cb = e >> 5;
-    const int hh = (int)((e >> 4) & 1), g = (int)(e & 15);
-    const int64_t c = cb * 32 + (g & 3) + 8 * (g >> 2) + 4 * hh;
-    v.cn32f[e] = c < k ? v.cn32[c] : 0x1.0p100f;
   }
 }
 

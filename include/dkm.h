@@ -48,6 +48,10 @@ extern "C" {
 #define DKM_MODE_SCREEN_BF16X3 3 /* same, x.c from bf16 hi/lo splits on the
                                bf16 MFMA (hi*hi + hi*lo + lo*hi); its own
                                bound; labels identical to EXACT.            */
+#define DKM_MODE_SCREEN_BF16 4 /* same, one bf16 product per term (hi*hi):
+                               a third of the matrix work, a looser bound;
+                               the candidates it leaves are re-checked with
+                               the EXACT arithmetic.  Labels identical.     */
 
 /* sum-dtype flags for dkm_update_centers (reference keeps X's dtype for the
  * partial sums; base.py:178 and :147) */

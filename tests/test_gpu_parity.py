@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 RTOL64 = 1e-9
 RTOL32 = 1e-4
-MODES = ["exact", "screen32", "bf16x3"]
+MODES = ["exact", "screen32", "bf16x3", "bf16"]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -274,7 +274,8 @@ def _partial_sum_gpu(x, C, mode):
     _device.partial_sum(dd, Ct, ws, lab, acc,
                         {"exact": _lib.MODE_EXACT,
                          "screen32": _lib.MODE_SCREEN32,
-                         "bf16x3": _lib.MODE_BF16X3}[mode])
+                         "bf16x3": _lib.MODE_BF16X3,
+                         "bf16": _lib.MODE_BF16}[mode])
     a = acc.cpu().numpy()
     return lab.cpu().numpy(), a[:k * d].reshape(k, d), a[k * d:], \
         _device.rechecked(ws)
@@ -304,7 +305,7 @@ def test_partial_sum_vs_oracle(mode, n, d, k, seed):
     _close(sums, rs, 1e-12)
 
 
-@pytest.mark.parametrize("mode", ["screen32", "bf16x3"])
+@pytest.mark.parametrize("mode", ["screen32", "bf16x3", "bf16"])
 def test_screen_rechecks_only_ambiguous_samples(mode):
     rng = np.random.default_rng(21)
     x = rng.standard_normal((200000, 32)) * 3
@@ -312,10 +313,11 @@ def test_screen_rechecks_only_ambiguous_samples(mode):
     lab, _, _, nre = _partial_sum_gpu(x, C, mode)
     rl = np.argmin(orc.dense_distances(x[:20000], C), axis=1)
     assert np.array_equal(lab[:20000], rl)
-    assert nre < 0.05 * x.shape[0]
+    # unclustered data: the single product (bound ~2^-8) leaves about half
+    assert nre < (0.6 if mode == "bf16" else 0.05) * x.shape[0]
 
 
-@pytest.mark.parametrize("mode", ["screen32", "bf16x3"])
+@pytest.mark.parametrize("mode", ["screen32", "bf16x3", "bf16"])
 @pytest.mark.parametrize("scale", [1e-30, 1e-3, 1.0, 1e3, 1e12])
 def test_screen_near_ties_across_scales(mode, scale):
     """Samples placed on (and 1e-6..1e-15 relative off) the bisector of two
@@ -338,7 +340,7 @@ def test_screen_near_ties_across_scales(mode, scale):
     assert np.array_equal(lab, orc.predict_labels(x, C))
 
 
-@pytest.mark.parametrize("mode", ["screen32", "bf16x3"])
+@pytest.mark.parametrize("mode", ["screen32", "bf16x3", "bf16"])
 def test_screen_forced_ties_go_to_exact_path(mode):
     # every sample equidistant (exactly) from centres 0 and 1
     rng = np.random.default_rng(3)
@@ -430,7 +432,7 @@ def test_assign_delta_equals_difference_of_partial_sums(mode, d, k):
     acc = torch.zeros(k * (d + 1), dtype=torch.float64, device=dev)
     lab = torch.from_numpy(prev.copy()).to(dev)
     m = {"exact": _lib.MODE_EXACT, "screen32": _lib.MODE_SCREEN32,
-         "bf16x3": _lib.MODE_BF16X3}[mode]
+         "bf16x3": _lib.MODE_BF16X3, "bf16": _lib.MODE_BF16}[mode]
     _device.prepare(Ct, ws, acc)
     _device.assign_delta(dd, Ct, ws, lab, acc, m)
     new = lab.cpu().numpy()
@@ -478,7 +480,7 @@ def test_fit_delta_refresh_matches_oracle(refresh):
     _close(km.centers, ref.centers, RTOL64)
 
 
-@pytest.mark.parametrize("mode", ["screen32", "bf16x3"])
+@pytest.mark.parametrize("mode", ["screen32", "bf16x3", "bf16"])
 @pytest.mark.parametrize("n,d,k", [(1_000_000, 32, 100), (200_000, 64, 1000)])
 def test_screen_stress_vs_exact_kernel(mode, n, d, k):
     """1M samples x 2 repetitions against the exact kernel on the same
@@ -500,7 +502,8 @@ def test_screen_stress_vs_exact_kernel(mode, n, d, k):
     ref = torch.empty(n, dtype=torch.int32, device="cuda")
     _device.prepare(C, ws, acc)
     _device.predict(dd, C, ws, ref, _lib.MODE_EXACT)
-    m = {"screen32": _lib.MODE_SCREEN32, "bf16x3": _lib.MODE_BF16X3}[mode]
+    m = {"screen32": _lib.MODE_SCREEN32, "bf16x3": _lib.MODE_BF16X3,
+         "bf16": _lib.MODE_BF16}[mode]
     for rep in range(2):
         lab = torch.full((n,), -7, dtype=torch.int32, device="cuda")
         _device.prepare(C, ws, acc)

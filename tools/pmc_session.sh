@@ -7,7 +7,7 @@ TAG=${1:-r01}; TARGET=${2:-bench}; shift 2
 OUT=gpurun_out/${TAG}_pmc; mkdir -p $OUT; export TMPDIR=/tmp
 N=${PMC_N:-20000000}
 if [ "$TARGET" = bench ]; then
-  PROG=(python bench.py --n $N --steps 8 --warmup 4 --no-cpu)
+  PROG=(python bench.py --n $N --steps 8 --warmup 4 --no-cpu --only-headline $BENCH_ARGS)
 else
   PROG=(python tools/bench_modes.py --n $N --rounds 2 --modes $TARGET)
 fi
