@@ -484,7 +484,11 @@ constexpr int SB = DKM_SB;  // screen block: SB/64 waves share one LDS image
 
 // A/B switches, compile-time only (variants.sh -DDKM_AB_...=1; all off in the
 // product build): no W32 screen, delta sums always / never by k_label_sums,
-// no per-wave undecided lists.
+// no per-wave undecided lists, post-screen sums by k_label_sums instead of
+// the sorted sums.
+#ifndef DKM_AB_LABEL_SUMS
+#define DKM_AB_LABEL_SUMS 0
+#endif
 #ifndef DKM_AB_NO_W32
 #define DKM_AB_NO_W32 0
 #endif
@@ -498,7 +502,8 @@ constexpr int SB = DKM_SB;  // screen block: SB/64 waves share one LDS image
 #define DKM_AB_NO_LIST 0
 #endif
 constexpr bool AB_NO_W32 = DKM_AB_NO_W32, AB_DELTA_POST = DKM_AB_DELTA_POST,
-               AB_NO_POST = DKM_AB_NO_POST, AB_NO_LIST = DKM_AB_NO_LIST;
+               AB_NO_POST = DKM_AB_NO_POST, AB_NO_LIST = DKM_AB_NO_LIST,
+               AB_LABEL_SUMS = DKM_AB_LABEL_SUMS;
 
 // Eight consecutive features t0..t0+7 of one row, as fp64.  VEC: d % 8 == 0
 // and 16-B aligned rows, so the 8 features are in range iff t0 < d.
@@ -2240,6 +2245,19 @@ static int launch_label_sums(const TX *X, int64_t lo, int64_t hi, int d,
   return check_launch("label sums");
 }
 
+// Sums from finished labels: the counting sort + segmented sums of
+// dkm_sums.hip when its scratch holds the range (k <= SORT_KMAX), else
+// k_label_sums.  AB_LABEL_SUMS (A/B builds) forces k_label_sums.
+template <class TX>
+static int launch_post_sums(const TX *X, int64_t lo, int64_t hi, int d,
+                            int64_t ldx, const int32_t *lab,
+                            const int32_t *prev, int k, double *acc,
+                            const WsView &v, hipStream_t s) {
+  if (!AB_LABEL_SUMS && sorted_sums_ok(k, hi - lo, v))
+    return sorted_sums<TX>(X, lo, hi, d, ldx, lab, prev, k, acc, v, s);
+  return launch_label_sums<TX>(X, lo, hi, d, ldx, lab, prev, k, acc, s);
+}
+
 // Do the [sums | counts] of k x d fit block-private LDS beside the screen's
 // fragments (else the screens write labels and k_label_sums sums)?
 static bool sums_fit_lds(int64_t k, int64_t d) {
@@ -2309,9 +2327,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                          int64_t ldx, const double *C, int k, const WsView &v,
                          size_t wsb, int32_t *labels, double *acc,
                          int acc_kind, hipStream_t s) {
-  const size_t fixed = (size_t)((const char *)v.queue - (const char *)v.hdr);
-  const int64_t nq =
-      std::min<int64_t>((int64_t)((wsb - fixed) / 4), INT32_MAX);
+  (void)wsb;
+  const int64_t nq = std::min<int64_t>(v.nq, INT32_MAX);
   if (!labels && nq < 1)
     return fail(DKM_E_WORKSPACE, "screen: no label scratch");
   const int64_t chunk = labels ? n : nq;
@@ -2388,8 +2405,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
     if ((r = launch_recheck<TX>(X, end, d, ldx, k, v, lab_out, acc,
                                 skind, vec, base, s)))
       return r;
-    if (post && (r = launch_label_sums<TX>(X, base, end, d, ldx, lab_out,
-                                           prevbuf, k, acc, s)))
+    if (post && (r = launch_post_sums<TX>(X, base, end, d, ldx, lab_out,
+                                          prevbuf, k, acc, v, s)))
       return r;
   }
   return 0;
@@ -2405,9 +2422,8 @@ static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
                        const double *C, int k, const WsView &v, size_t wsb,
                        int32_t *labels, double *acc, int acc_kind,
                        hipStream_t s) {
-  const size_t fixed = (size_t)((const char *)v.queue - (const char *)v.hdr);
-  const int64_t nq =
-      std::min<int64_t>((int64_t)((wsb - fixed) / 4), INT32_MAX);
+  (void)wsb;
+  const int64_t nq = std::min<int64_t>(v.nq, INT32_MAX);
   if (!labels && nq < 1)
     return fail(DKM_E_WORKSPACE, "gemm: no label scratch");
   const int64_t chunk = labels ? n : nq;
@@ -2427,8 +2443,8 @@ static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
     int r = gemm_screen<TX>(X, base, end, d, ldx, C, k, v, lab_out,
                             skind ? acc : nullptr, skind == 2, s);
     if (r) return r;
-    if (post && (r = launch_label_sums<TX>(X, base, end, d, ldx, lab_out,
-                                           prevbuf, k, acc, s)))
+    if (post && (r = launch_post_sums<TX>(X, base, end, d, ldx, lab_out,
+                                          prevbuf, k, acc, v, s)))
       return r;
   }
   return 0;

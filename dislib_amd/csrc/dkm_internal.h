@@ -34,9 +34,11 @@ struct WsHeader {
   uint64_t rechecked_total; // diagnostics
   uint32_t gcount;          // GEMM screen: candidate-list entries (per chunk)
   uint32_t gcount2;         // GEMM screen: full-scan entries (per chunk)
-  uint64_t reserved[7];
+  int32_t nmoved;           // sorted sums: samples whose label changed
+  uint32_t pad1;
+  uint64_t reserved[6];
 };
-constexpr uint64_t WS_MAGIC = 0x444b4d5753303032ull;  // "DKMWS002"
+constexpr uint64_t WS_MAGIC = 0x444b4d5753303033ull;  // "DKMWS003"
 constexpr size_t WS_HDR = 256;
 
 __host__ __device__ inline int64_t round_up(int64_t a, int64_t b) {
@@ -111,8 +113,25 @@ struct WsView {
   float *gxn;      // gemm_chunk fp32 upper bounds of ||x||
   int2 *gpart;     // gemm_chunk x kpad256/GT x GTOP (score bits, centre)
   int64_t gchunk;  // samples per split chunk
-  int32_t *queue; // n_queue sample indices for the exact re-check
+  // sorted sums (dkm_sums.hip; k <= SORT_KMAX, else NULL)
+  int32_t *soff;   // k + 1 cluster offsets into sitems
+  int32_t *scur;   // k scatter cursors
+  int32_t *scnt;   // k counts
+  // the tail: three arrays of nq entries
+  int64_t nq;
+  int32_t *queue; // label scratch / previous labels / re-check indices
+  int32_t *sitems; // sample indices grouped by cluster
+  int32_t *smoved; // samples whose label changed (delta sums)
 };
+
+// Sorted sums: counting sort of the sample indices by label (LDS histograms
+// of k bins: k <= SORT_KMAX), then segmented row sums.
+constexpr int SORT_KMAX = 16384;
+bool sorted_sums_ok(int64_t k, int64_t n, const WsView &v);
+template <class TX>
+int sorted_sums(const TX *X, int64_t lo, int64_t hi, int d, int64_t ldx,
+                const int32_t *lab, const int32_t *prev, int k, double *acc,
+                const WsView &v, hipStream_t s);
 
 // Per-wave lists of the screen's undecided samples (resolved by
 // k_recheck_list without scanning the labels): one segment of TL_CAP

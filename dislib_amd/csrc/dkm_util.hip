@@ -67,7 +67,8 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
     b += (size_t)B1_SEGS * B1_CAP * 8;              // clist
     b += (size_t)B1_SEGS * 4;                       // ccount
   }
-  b += round_up(n_queue * 4, 256);    // queue
+  if (k <= SORT_KMAX) b += round_up((k + 1) * 4, 256) + 2 * round_up(k * 4, 256);
+  b += 3 * round_up(n_queue * 4, 256);  // queue, sitems, smoved
   return b;
 }
 
@@ -130,10 +131,22 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
     v->ccount = (int32_t *)p;
     p += (size_t)B1_SEGS * 4;
   }
-  v->queue = (int32_t *)p;
+  v->soff = v->scur = v->scnt = nullptr;
+  if (k <= SORT_KMAX) {
+    v->soff = (int32_t *)p;
+    p += round_up((k + 1) * 4, 256);
+    v->scur = (int32_t *)p;
+    p += round_up(k * 4, 256);
+    v->scnt = (int32_t *)p;
+    p += round_up(k * 4, 256);
+  }
   const size_t fixed = (size_t)(p - (char *)ws);
-  if (bytes < fixed + 256)
+  if (bytes < fixed + 768)
     return fail(DKM_E_WORKSPACE, "workspace too small for k/d");
+  v->nq = (int64_t)((bytes - fixed) / 12) / 64 * 64;
+  v->queue = (int32_t *)p;
+  v->sitems = v->queue + v->nq;
+  v->smoved = v->sitems + v->nq;
   return 0;
 }
 
@@ -388,9 +401,7 @@ int dkm_prepare_centers(const double *C, int64_t k, int64_t d, int flags,
   if (int r = ws_view(ws, ws_b, k, d, &v)) return r;
   hipStream_t s = (hipStream_t)stream;
   const int64_t dpad = round_up(d, 4);
-  const size_t fixed = (size_t)((char *)v.queue - (char *)ws);
-  const int64_t nq = (int64_t)((ws_b - fixed) / 4);
-  k_ws_header<<<1, 64, 0, s>>>(v.hdr, k, d, dpad, nq);
+  k_ws_header<<<1, 64, 0, s>>>(v.hdr, k, d, dpad, v.nq);
   k_prepare<<<(unsigned)k, 256, 0, s>>>(C, k, d, dpad, flags, v);
   {
     const int64_t tot = (kpad16(k) / 16) * (dpad32(d) / 32) * 512;
