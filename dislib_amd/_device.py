@@ -197,9 +197,15 @@ def partial_sum(dd, C, ws, labels, acc, mode):
 
 
 def assign_delta(dd, C, ws, labels, delta, mode):
-    """Incremental assignment (dense only): labels in/out, delta +=."""
+    """Incremental assignment: labels in/out, delta +=."""
     so = _lib.lib()
     k = C.shape[0]
+    if dd.sparse:
+        _lib.check(so.dkm_assign_delta_csr_f64(
+            ptr(dd.indptr), ptr(dd.indices), ptr(dd.data), dd.n, dd.d,
+            ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(delta),
+            stream_ptr()), "dkm_assign_delta_csr_f64")
+        return
     fn = so.dkm_assign_delta_f32 if dd.dtype == np.float32 else \
         so.dkm_assign_delta_f64
     _lib.check(fn(ptr(dd.X), dd.n, dd.d, dd.X.stride(0), ptr(C), k, ws.p,

@@ -47,6 +47,8 @@ SIGNATURES = {
                                   _p]),
     "dkm_partial_sum_csr_f64": (_i32, [_p, _p, _p, _i64, _i64, _p, _i64, _p,
                                        _sz, _p, _p, _p]),
+    "dkm_assign_delta_csr_f64": (_i32, [_p, _p, _p, _i64, _i64, _p, _i64,
+                                        _p, _sz, _p, _p, _p]),
     "dkm_predict_csr_f64": (_i32, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _sz,
                                    _p, _p]),
     "dkm_make_blobs_f64": (_i32, [_p, _i64, _i64, _i64, _i64, _u64, _f64,

@@ -154,9 +154,9 @@ class _Lloyd:
     ``step()`` is one Lloyd iteration: prepare -> fused assignment (HIP) ->
     all-reduce of the per-rank buffer (RCCL when N > 1) -> centre update +
     criterion (HIP) -> one 4-byte flag read (the reference's per-iteration
-    sync, base.py:143).  Dense data uses the incremental assignment
-    (dkm_assign_delta: only samples whose label changed move their row
-    between clusters) and recomputes ``state`` from scratch
+    sync, base.py:143).  The fit uses the incremental assignment
+    (dkm_assign_delta*: only samples whose label changed move their row
+    between clusters; dense and CSR) and recomputes ``state`` from scratch
     (dkm_partial_sum) on the first and every REFRESH-th iteration, which
     bounds the rounding drift of the running sums."""
 
@@ -206,7 +206,7 @@ class _Lloyd:
             prepare(self.C, self.ws, self.acc, csr=self.sparse)
 
     def _full(self):
-        return self.sparse or self.it % self.refresh == 0
+        return self.it % self.refresh == 0
 
     def partial(self):
         """The hot kernel: fused assignment over all resident samples, full

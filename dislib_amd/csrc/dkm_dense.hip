@@ -635,7 +635,7 @@ __device__ __forceinline__ bool resolve_lane(
 #pragma unroll 1
     for (int jc = 0; jc < k; ++jc) {
       if (sane && !(score(jc) <= lim)) continue;
-      const SqDiffT<TX> f{xr, ct64 + jc, (int64_t)k};
+      const SqDiffT<TX> f{xr, ct64 + jc, ct_ld(k)};
       const double dist = sqrt(pw_leaf(f, 0, d));
       if (dist < best || bi < 0) {
         best = dist;
@@ -1874,7 +1874,7 @@ __global__ void __launch_bounds__(BLOCK)
       double best = INFINITY;
       int bi = 0x7fffffff;  // lanes without a centre never win
       for (int jc = lane; jc < k; jc += 64) {
-        const SqDiffT<TX> f{xr, v.ct64 + jc, (int64_t)k};
+        const SqDiffT<TX> f{xr, v.ct64 + jc, ct_ld(k)};
         const double dist = sqrt(SMALL ? pw_leaf(f, 0, d) : pw_sum(f, d));
         if (dist < best || bi == 0x7fffffff) {
           best = dist;

@@ -674,7 +674,7 @@ __global__ void __launch_bounds__(1024)
     int lab = 0x7fffffff;  // lanes without a centre never win
     for (int jc = threadIdx.x; jc < k; jc += 1024) {
       const double dist =
-          sqrt(pw_sum(SqDiffT<TX>{xr, v.ct64 + jc, (int64_t)k}, d));
+          sqrt(pw_sum(SqDiffT<TX>{xr, v.ct64 + jc, ct_ld(k)}, d));
       if (nan_first_less(dist, jc, best, lab)) {
         best = dist;
         lab = jc;

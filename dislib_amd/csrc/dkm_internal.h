@@ -36,7 +36,9 @@ struct WsHeader {
   uint32_t gcount2;         // GEMM screen: full-scan entries (per chunk)
   int32_t nmoved;           // sorted sums: samples whose label changed
   uint32_t pad1;
-  uint64_t reserved[6];
+  uint32_t csr_nund;        // CSR screen: undecided samples of this chunk
+  uint32_t pad2;
+  uint64_t reserved[5];
 };
 constexpr uint64_t WS_MAGIC = 0x444b4d5753303033ull;  // "DKMWS003"
 constexpr size_t WS_HDR = 256;
@@ -55,6 +57,11 @@ constexpr int GSTAGE = GT * GBK * 4;    // bytes per operand tile per stage
 constexpr int GTOP = 4;                 // (score, centre) pairs kept per sample
 
 __host__ __device__ inline int64_t kpad256(int64_t k) { return (k + 255) / 256 * 256; }
+
+// Row stride (elements) of the transposed centres C^T (d x ct_ld(k)): 128-B
+// aligned rows, so the CSR kernels' 32-centre slices are whole lines and
+// their 16-B loads aligned.  Padding columns are never read into a result.
+__host__ __device__ inline int64_t ct_ld(int64_t k) { return (k + 15) / 16 * 16; }
 
 // ---------------------------------------------------------------------------
 // Single-product screen (k_screen_b1, dkm_dense.hip): bf16 hi of x and -2c
@@ -94,7 +101,8 @@ struct WsView {
   float *c32;     // k x dpad fp32 centres (zero padded)
   float *cn32;    // k fp32 ||c||^2 (computed in fp64, rounded once)
   double *cn64;   // k fp64 ||c||^2, sequential over t (sklearn row_norms)
-  double *ct64;   // d x k transposed centres (DKM_PREP_CSR)
+  double *ct64;   // d x ct_ld(k) transposed centres (exact re-checks, CSR)
+  float *ct32;    // d x ct_ld(k) fp32 transposed centres (CSR screen)
   float *cfrag;   // fp32 -2*centres in MFMA A-fragment order (dkm_dense)
   float *cnpad;   // kpad16 fp32 ||c||^2, 2^100 for padding centres
   uint16_t *bfrag; // bf16 hi/lo of -2*centres, 16x16x32 fragment order
@@ -132,6 +140,11 @@ template <class TX>
 int sorted_sums(const TX *X, int64_t lo, int64_t hi, int d, int64_t ldx,
                 const int32_t *lab, const int32_t *prev, int k, double *acc,
                 const WsView &v, hipStream_t s);
+
+// Sample indices [lo, hi) grouped by lab[i] (counting sort) into v.sitems,
+// cluster c at [v.soff[c], v.soff[c + 1]) (the CSR sums, dkm_sparse.hip).
+int sort_by_label(const int32_t *lab, int64_t lo, int64_t hi, int k,
+                  const WsView &v, hipStream_t s);
 
 // Per-wave lists of the screen's undecided samples (resolved by
 // k_recheck_list without scanning the labels): one segment of TL_CAP

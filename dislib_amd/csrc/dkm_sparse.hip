@@ -11,48 +11,308 @@
 //   yy_j  = sequential sum of C[j][t]^2 over t (stored entries; exact zeros
 //           add nothing)
 //   dist_j = sqrt(max(0, ((-2 * dot_j) + xx) + yy_j))
-// followed by np.argmin (first index).  This kernel reproduces that
-// arithmetic bit-for-bit.
+// followed by np.argmin (first index).  Labels are bit-exact: a sample is
+// labelled by the screen below only when a rigorous bound proves the
+// reference arithmetic picks the same centre, otherwise by that arithmetic.
 //
-// Layout: one wave per sample, lanes over centres j = lane, lane+64, ...;
-// the centres are read transposed (C^T, d x k, built by dkm_prepare_centers
-// with DKM_PREP_CSR) so that the 64 lanes of a stored column read 512
-// contiguous bytes.  Sums are added with fp64 atomics (lanes over the
-// sample's stored entries).
+// The time goes into gathering nnz rows of C^T per sample (k values each:
+// 10 KB in fp32 at C5, k = 256, 10 nnz) from a table no L2 holds whole.
+// So the centres are cut into S slices (S = 1, 2, 4 or 8) small enough for
+// one XCD's 4 MB L2, and block b works on slice b % S: blocks b and b + 8
+// share an XCD, so each XCD gathers from its own slice only (a speed
+// assumption, never a correctness one).
+//   k_csr_screen   8 lanes per sample (8 samples per wave), 4 centres per
+//                  lane per 32-centre pass, 16-B loads of the fp32 C^T
+//                  (d x ct_ld(k)); the row's entries staged 8 at a time in
+//                  the group's lanes and walked by ds_bpermute.  Per centre
+//                  j: s_j = |c_j|^2 - 2 x.c_j (fp32 fma chain), the bound
+//                  B_j from sum |x||c_j| (below), and the slice's state
+//                  (s1, s1 - B1, s1 + B1, c1, min over others of s_j - B_j).
+//   k_csr_merge    one lane per sample: the slices' states merged (ascending
+//                  centre ranges: a strict < keeps the first index); decided
+//                  when s1 + B1 < s_j - B_j for every other j -- then the
+//                  reference's fp64 distances order the same way, strictly,
+//                  also after sqrt -- else listed for k_csr_resolve.  Writes
+//                  the label and, on the incremental path, moves the rows
+//                  whose label changed (+x new, -x previous; fp64 atomics).
+//   k_csr_resolve  a wave per listed sample: the reference arithmetic over
+//                  all k centres (fp64 C^T), first-index argmin.
+//   k_csr_seg_sums the full [sums | counts]: samples counting-sorted by
+//                  label (dkm_sums.hip), a block per 4096 sorted positions
+//                  adds rows into an LDS copy of the cluster's sum (fp64 LDS
+//                  atomics) and flushes it once per cluster segment.
+// Samples are processed in chunks so that the S slice states fit the
+// workspace tail (20 bytes per slice and sample).
+//
+// The bound.  With u = 2^-24 (fp32) and w = 2^-53 (fp64), n stored entries,
+// A_j >= sum |x_v c_jv| (accumulated beside the dot) and M_j = xx + |c_j|^2
+// + 2 A_j + |s_j| >= the magnitude of every partial result:
+//   fp32 dot vs exact          (n + 2) u A_j     (inputs rounded, fma chain)
+//   sklearn's fp64 dot         n w A_j
+//   s_j rounding, |c|^2 -> fp32  u |s_j| + u |c_j|^2
+//   sklearn's two additions    2 w M_j;  sqrt strictly monotone: 4 w M_j
+// B_j = 2 x their sum (+ 2^-100 absolute, for underflow): s1 + B1 < s_j - B_j
+// implies S_1 < S_j with a margin that survives sqrt, where S = sklearn's
+// squared distances.  NaN/inf anywhere makes a sample undecided.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <string>
 
 #include "dkm_internal.h"
 
-// A/B switch (variants.sh): the per-centre-group kernel for every k
-#ifndef DKM_AB_CSR_OLD
-#define DKM_AB_CSR_OLD 0
-#endif
-
 namespace dkm {
 
-__global__ void __launch_bounds__(256)
-    k_csr_assign(const int64_t *__restrict__ indptr,
+namespace {
+
+constexpr int CSR_BLOCK = 256;
+constexpr int CSR_G = 8;                   // lanes per sample
+constexpr int CSR_SPW = WAVE / CSR_G;      // samples per wave
+constexpr int CSR_PASS = 4 * CSR_G;        // centres per pass (4 per lane)
+constexpr size_t CSR_SLICE_BYTES = 2u << 20;  // fp32 C^T slice per XCD L2
+constexpr int CSR_SEGP = 4096;             // sorted positions per sums block
+constexpr int CSR_TD = 16384;              // sums columns per LDS tile
+constexpr int CSR_SUMB = 1024;
+
+enum { OP_PREDICT = 0, OP_FULL = 1, OP_DELTA = 2, OP_FULL_ATOMIC = 3 };
+
+struct SliceState {
+  float s1, lo1, hi1, lo2;
+};
+
+__device__ __forceinline__ int lane_prefix64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+__device__ __forceinline__ void add_row(const int64_t *indptr,
+                                        const int32_t *indices,
+                                        const double *data, int64_t i, int c,
+                                        int d, int k, double sign,
+                                        double *acc) {
+  const int64_t a = indptr[i], b = indptr[i + 1];
+  for (int64_t v = a; v < b; ++v)
+    atomic_add_f64(acc + (int64_t)c * d + indices[v], sign * data[v]);
+  atomic_add_f64(acc + (int64_t)k * d + c, sign);
+}
+
+}  // namespace
+
+// NP passes of 32 centres per walk over the entries (a slice wider than
+// 32 * NP centres is walked again).  Slice s covers centres
+// [s * ks, min(k, (s + 1) * ks)), ks a multiple of 32.
+template <int NP>
+__global__ void __launch_bounds__(CSR_BLOCK)
+    k_csr_screen(const int64_t *__restrict__ indptr,
                  const int32_t *__restrict__ indices,
-                 const double *__restrict__ data, int64_t n, int d,
-                 const double *__restrict__ CT, const double *__restrict__ yy,
-                 int k, int32_t *labels, double *acc) {
+                 const double *__restrict__ data, int64_t i0, int64_t m,
+                 const float *__restrict__ CT, int64_t ldct,
+                 const float *__restrict__ cn, int k, int S, int ks,
+                 SliceState *__restrict__ pst, int32_t *__restrict__ pidx,
+                 float *__restrict__ pxx) {
+  const int lane = threadIdx.x & 63, sg = lane / CSR_G, gl = lane % CSR_G;
+  const int gbase = sg * CSR_G;
+  const int s = blockIdx.x % S;
+  const int64_t stream = blockIdx.x / S, nstream = gridDim.x / S;
+  const int64_t wv = stream * (CSR_BLOCK / 64) + (threadIdx.x >> 6);
+  const int64_t nwv = nstream * (CSR_BLOCK / 64);
+  const int j_lo = s * ks, j_hi = min(k, j_lo + ks);
+  for (int64_t q0 = wv * CSR_SPW; q0 < m; q0 += nwv * CSR_SPW) {
+    const int64_t q = q0 + sg;
+    const bool live = q < m;
+    const int64_t a = live ? indptr[i0 + q] : 0;
+    const int64_t b = live ? indptr[i0 + q + 1] : 0;
+    const float nf = (float)(b - a);
+    SliceState st{INFINITY, INFINITY, INFINITY, INFINITY};
+    int i1 = 0x7fffffff;
+    float xx = 0.f;
+    for (int jp = j_lo; jp < j_hi; jp += CSR_PASS * NP) {
+      float dot[NP][4], adot[NP][4];
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) dot[p][h] = adot[p][h] = 0.f;
+      const bool first = jp == j_lo;
+      for (int64_t c0 = a; c0 < b; c0 += CSR_G) {
+        const int cnt = (int)min<int64_t>(CSR_G, b - c0);
+        int myi = 0;
+        float myv = 0.f;
+        if (gl < cnt) {
+          myi = indices[c0 + gl];
+          myv = (float)data[c0 + gl];
+        }
+        // the chunk's C^T row loads first, then the adds
+        float4 cv[CSR_G][NP];
+        float vv[CSR_G];
+#pragma unroll
+        for (int e = 0; e < CSR_G; ++e) {
+          const int idx = __shfl(myi, gbase + e, WAVE);
+          vv[e] = __shfl(myv, gbase + e, WAVE);
+          const float *row = CT + (int64_t)idx * ldct + jp + 4 * gl;
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            const int j = jp + CSR_PASS * p + 4 * gl;
+            cv[e][p] = (e < cnt && j < j_hi)
+                           ? *(const float4 *)(row + CSR_PASS * p)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < CSR_G; ++e) {
+          if (e < cnt) {
+            const float v = vv[e], av = fabsf(v);
+            if (first) xx = fmaf(v, v, xx);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+              const float c4[4] = {cv[e][p].x, cv[e][p].y, cv[e][p].z,
+                                   cv[e][p].w};
+#pragma unroll
+              for (int h = 0; h < 4; ++h) {
+                dot[p][h] = fmaf(v, c4[h], dot[p][h]);
+                adot[p][h] = fmaf(av, fabsf(c4[h]), adot[p][h]);
+              }
+            }
+          }
+        }
+      }
+      const float xx_up = xx * (1.f + (nf + 4.f) * 0x1.0p-23f);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int j = jp + CSR_PASS * p + 4 * gl + h;
+          if (j < j_hi) {
+            const float cj = cn[j];
+            const float sj = fmaf(-2.f, dot[p][h], cj);
+            const float as = fabsf(sj), A = adot[p][h];
+            const float M = xx_up + cj + 2.f * A + as;
+            const float B = 0x1.0p-23f * (cj + as + 2.f * (nf + 2.f) * A) +
+                            (2.f * nf + 6.f) * 0x1.0p-52f * M + 0x1.0p-100f;
+            float lo = sj - B;
+            const float hi = sj + B;
+            if (!(lo == lo) || !(hi < INFINITY)) lo = -INFINITY;  // poison
+            if (sj < st.s1) {
+              st.lo2 = fminf(st.lo2, st.lo1);
+              st.s1 = sj;
+              st.lo1 = lo;
+              st.hi1 = hi;
+              i1 = j;
+            } else {
+              st.lo2 = fminf(st.lo2, lo);
+            }
+          }
+        }
+      }
+    }
+    // a lane whose centres were all NaN keeps i1 = none: poison the slice
+    if (j_lo < j_hi && i1 == 0x7fffffff) st.lo2 = -INFINITY;
+#pragma unroll
+    for (int off = CSR_G / 2; off >= 1; off >>= 1) {
+      SliceState o;
+      o.s1 = __shfl_xor(st.s1, off, WAVE);
+      o.lo1 = __shfl_xor(st.lo1, off, WAVE);
+      o.hi1 = __shfl_xor(st.hi1, off, WAVE);
+      o.lo2 = __shfl_xor(st.lo2, off, WAVE);
+      const int oi = __shfl_xor(i1, off, WAVE);
+      const bool take = o.s1 < st.s1 || (o.s1 == st.s1 && oi < i1);
+      if (take) {
+        o.lo2 = fminf(fminf(o.lo2, st.lo2), st.lo1);
+        st = o;
+        i1 = oi;
+      } else {
+        st.lo2 = fminf(fminf(st.lo2, o.lo2), o.lo1);
+      }
+    }
+    if (live && gl == 0) {
+      pst[(int64_t)s * m + q] = st;
+      pidx[(int64_t)s * m + q] = i1;
+      if (s == 0) pxx[q] = xx * (1.f - (nf + 4.f) * 0x1.0p-23f);
+    }
+  }
+}
+
+// One lane per sample: merge the slices, decide, write the label, list the
+// undecided, move the rows.
+__global__ void __launch_bounds__(256)
+    k_csr_merge(const int64_t *__restrict__ indptr,
+                const int32_t *__restrict__ indices,
+                const double *__restrict__ data, int64_t i0, int64_t m, int d,
+                int k, int S, const SliceState *__restrict__ pst,
+                const int32_t *__restrict__ pidx,
+                const float *__restrict__ pxx, int32_t *labels, double *acc,
+                int op, int32_t *__restrict__ list, uint32_t *nlist) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t q0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63);
+       q0 < m; q0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t q = q0 + lane;
+    bool und = false;
+    if (q < m) {
+      SliceState w = pst[q];
+      int wi = pidx[q];
+      float L = w.lo2;
+      for (int s = 1; s < S; ++s) {
+        const SliceState t = pst[(int64_t)s * m + q];
+        const int ti = pidx[(int64_t)s * m + q];
+        if (ti != 0x7fffffff &&
+            (wi == 0x7fffffff || t.s1 < w.s1 || (t.s1 == w.s1 && ti < wi))) {
+          L = fminf(fminf(L, w.lo1), t.lo2);
+          w = t;
+          wi = ti;
+        } else {
+          L = fminf(fminf(L, t.lo1), t.lo2);
+        }
+      }
+      const bool decided =
+          wi != 0x7fffffff && w.hi1 < L && pxx[q] + L > 0.f;
+      const int64_t i = i0 + q;
+      const int prev = (op == OP_DELTA) ? labels[i] : -1;
+      if (decided) {
+        if (labels && !(op == OP_DELTA && prev == wi)) labels[i] = wi;
+        if (op == OP_FULL_ATOMIC || (op == OP_DELTA && prev != wi)) {
+          add_row(indptr, indices, data, i, wi, d, k, 1.0, acc);
+          if (op == OP_DELTA && prev >= 0 && prev < k)
+            add_row(indptr, indices, data, i, prev, d, k, -1.0, acc);
+        }
+      } else {
+        und = true;
+        if (labels) labels[i] = -(prev + 2);
+      }
+    }
+    const uint64_t mu = __ballot(und);
+    if (mu) {
+      int base = 0;
+      if (lane == 0) base = (int)atomicAdd(nlist, (uint32_t)__popcll(mu));
+      base = __shfl(base, 0, WAVE);
+      if (und) list[base + lane_prefix64(mu)] = (int32_t)q;
+    }
+  }
+}
+
+// A wave per undecided sample: the reference arithmetic over every centre.
+__global__ void __launch_bounds__(256)
+    k_csr_resolve(const int64_t *__restrict__ indptr,
+                  const int32_t *__restrict__ indices,
+                  const double *__restrict__ data, int64_t i0, int d,
+                  const double *__restrict__ CT, int64_t ldct,
+                  const double *__restrict__ yy, int k, int32_t *labels,
+                  double *acc, int op, const int32_t *__restrict__ list,
+                  const uint32_t *nlist, unsigned long long *total) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t i = wave; i < n; i += nwaves) {
+  const uint32_t cnt = *nlist;
+  if (wave == 0 && lane == 0 && cnt) atomicAdd(total, (unsigned long long)cnt);
+  for (int64_t e = wave; e < (int64_t)cnt; e += nwaves) {
+    const int64_t i = i0 + list[e];
     const int64_t a = indptr[i], b = indptr[i + 1];
-    double xx = 0.0;  // identical in every lane (broadcast loads)
+    double xx = 0.0;
     for (int64_t v = a; v < b; ++v) xx = xx + data[v] * data[v];
     double best = INFINITY;
     int bi = 0x7fffffff;
     for (int j = lane; j < k; j += 64) {
       double dot = 0.0;
       for (int64_t v = a; v < b; ++v)
-        dot = dot + data[v] * CT[(int64_t)indices[v] * k + j];
+        dot = dot + data[v] * CT[(int64_t)indices[v] * ldct + j];
       double dd = -2.0 * dot;
       dd = dd + xx;
       dd = dd + yy[j];
@@ -63,125 +323,187 @@ __global__ void __launch_bounds__(256)
       }
     }
     wave_argmin(best, bi);
+    if (bi == 0x7fffffff) bi = 0;  // k >= 1: unreachable
+    const int prev = (op == OP_DELTA) ? -labels[i] - 2 : -1;
     if (lane == 0 && labels) labels[i] = bi;
-    if (acc) {
-      for (int64_t v = a + lane; v < b; v += 64)
+    const bool add = op == OP_FULL_ATOMIC || (op == OP_DELTA && prev != bi);
+    if (add) {
+      for (int64_t v = a + lane; v < b; v += 64) {
         atomic_add_f64(acc + (int64_t)bi * d + indices[v], data[v]);
-      if (lane == 0) atomic_add_f64(acc + (int64_t)k * d + bi, 1.0);
+        if (op == OP_DELTA && prev >= 0 && prev < k)
+          atomic_add_f64(acc + (int64_t)prev * d + indices[v], -data[v]);
+      }
+      if (lane == 0) {
+        atomic_add_f64(acc + (int64_t)k * d + bi, 1.0);
+        if (op == OP_DELTA && prev >= 0 && prev < k)
+          atomic_add_f64(acc + (int64_t)k * d + prev, -1.0);
+      }
     }
   }
 }
 
-// Centres per lane known at compile time (k <= 64 * KPL): the row's stored
-// entries are loaded once, 64 at a time (lane e holds entry e), and walked
-// in order by readlane, so each entry's C^T row loads (512 B per 64
-// centres) issue back to back instead of behind an index load per centre
-// group.  Every centre's dot still runs over the entries in stored order
-// (product, then add), exactly as above.
-template <int KPL>
-__global__ void __launch_bounds__(256)
-    k_csr_assign_r(const int64_t *__restrict__ indptr,
+// Full sums over label-sorted samples: a block per CSR_SEGP positions and
+// column tile (blockIdx.y); 16 lanes per row add the row's entries into the
+// LDS copy of the current cluster's sum, flushed at each cluster change.
+__global__ void __launch_bounds__(CSR_SUMB)
+    k_csr_seg_sums(const int64_t *__restrict__ indptr,
                    const int32_t *__restrict__ indices,
-                   const double *__restrict__ data, int64_t n, int d,
-                   const double *__restrict__ CT, const double *__restrict__ yy,
-                   int k, int32_t *labels, double *acc) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t i = wave; i < n; i += nwaves) {
-    const int64_t a = indptr[i], b = indptr[i + 1];
-    double xx = 0.0;
-    double dot[KPL];
-#pragma unroll
-    for (int g = 0; g < KPL; ++g) dot[g] = 0.0;
-    for (int64_t c0 = a; c0 < b; c0 += 64) {
-      const int cnt = (int)std::min<int64_t>(64, b - c0);
-      int myi = 0;
-      double myv = 0.0;
-      if (lane < cnt) {
-        myi = indices[c0 + lane];
-        myv = data[c0 + lane];
-      }
-      const int64_t mv = __double_as_longlong(myv);
-#pragma unroll 4
-      for (int e = 0; e < cnt; ++e) {
-        const int idx = __builtin_amdgcn_readlane(myi, e);
-        const int lo = __builtin_amdgcn_readlane((int)(mv & 0xffffffff), e);
-        const int hi = __builtin_amdgcn_readlane((int)(mv >> 32), e);
-        const double val = __longlong_as_double(
-            ((int64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-        xx = xx + val * val;
-        const double *row = CT + (int64_t)idx * k;
-#pragma unroll
-        for (int g = 0; g < KPL; ++g) {
-          const int j = lane + 64 * g;
-          if (j < k) dot[g] = dot[g] + val * row[j];
-        }
+                   const double *__restrict__ data,
+                   const int32_t *__restrict__ sorted,
+                   const int32_t *__restrict__ off, int k, int d, int td,
+                   double *__restrict__ acc) {
+  extern __shared__ double lsum[];
+  const int64_t n = off[k];
+  const int64_t p0 = (int64_t)blockIdx.x * CSR_SEGP;
+  if (p0 >= n) return;
+  const int64_t p1 = std::min<int64_t>(n, p0 + CSR_SEGP);
+  const int col0 = blockIdx.y * td;
+  const int tw = min(td, d - col0);
+  for (int t = threadIdx.x; t < tw; t += CSR_SUMB) lsum[t] = 0.0;
+  int lo_c = 0, hi_c = k;  // off[lo_c] <= p0 < off[hi_c]
+  while (hi_c - lo_c > 1) {
+    const int mid = (lo_c + hi_c) >> 1;
+    if (off[mid] <= p0) lo_c = mid;
+    else hi_c = mid;
+  }
+  int c = lo_c;
+  const int sub = threadIdx.x & 15, row0 = threadIdx.x >> 4;
+  for (int64_t p = p0; p < p1;) {
+    while (off[c + 1] <= p) ++c;  // empty clusters
+    const int64_t e = std::min<int64_t>(p1, off[c + 1]);
+    __syncthreads();
+    for (int64_t r = p + row0; r < e; r += CSR_SUMB / 16) {
+      const int64_t i = sorted[r];
+      const int64_t a = indptr[i], b = indptr[i + 1];
+      for (int64_t v = a + sub; v < b; v += 16) {
+        const int t = indices[v] - col0;
+        if (t >= 0 && t < tw)
+          __hip_atomic_fetch_add(&lsum[t], data[v], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
-    double best = INFINITY;
-    int bi = 0x7fffffff;
-#pragma unroll
-    for (int g = 0; g < KPL; ++g) {
-      const int j = lane + 64 * g;
-      if (j < k) {
-        double dd = -2.0 * dot[g];
-        dd = dd + xx;
-        dd = dd + yy[j];
-        const double dist = sqrt(dd > 0.0 ? dd : 0.0);
-        if (dist < best || bi == 0x7fffffff) {
-          best = dist;
-          bi = j;
-        }
+    __syncthreads();
+    for (int t = threadIdx.x; t < tw; t += CSR_SUMB) {
+      const double x = lsum[t];
+      if (x != 0.0) {
+        atomic_add_f64(acc + (int64_t)c * d + col0 + t, x);
+        lsum[t] = 0.0;
       }
     }
-    wave_argmin(best, bi);
-    if (lane == 0 && labels) labels[i] = bi;
-    if (acc) {
-      for (int64_t v = a + lane; v < b; v += 64)
-        atomic_add_f64(acc + (int64_t)bi * d + indices[v], data[v]);
-      if (lane == 0) atomic_add_f64(acc + (int64_t)k * d + bi, 1.0);
-    }
+    if (threadIdx.x == 0 && blockIdx.y == 0)
+      atomic_add_f64(acc + (int64_t)k * d + c, (double)(e - p));
+    p = e;
   }
 }
 
-static int csr_assign(const int64_t *indptr, const int32_t *indices,
-                      const double *data, int64_t n, int64_t d,
-                      const double *C, int64_t k, const void *ws, size_t wsb,
-                      int32_t *labels, double *acc, void *stream,
-                      const char *who) {
+static int csr_cus() {
+  static thread_local int cached_dev = -1, n = 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return n;
+  if (dev != cached_dev) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) == hipSuccess) n = p.multiProcessorCount;
+    cached_dev = dev;
+  }
+  return n;
+}
+
+// slices: the fewest (power of two <= 8) whose fp32 C^T slice fits the
+// budget, never narrower than one 32-centre pass
+static int csr_slices(int64_t k, int64_t d) {
+  int S = 1;
+  while (S < 8 && (k + S - 1) / S > CSR_PASS &&
+         (size_t)(round_up((k + S - 1) / S, CSR_PASS) * d * 4) > CSR_SLICE_BYTES)
+    S *= 2;
+  return S;
+}
+
+static int csr_full_sums(const int64_t *indptr, const int32_t *indices,
+                         const double *data, int64_t n, int d, int k,
+                         const int32_t *labels, double *acc, const WsView &v,
+                         hipStream_t st) {
+  const int td = (int)std::min<int64_t>(round_up(d, 64), CSR_TD);
+  const unsigned ny = (unsigned)((d + td - 1) / td);
+  if (hipFuncSetAttribute((const void *)k_csr_seg_sums,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          CSR_TD * 8) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "csr sums: LDS attribute");
+  const int64_t span = std::min<int64_t>(v.nq, INT32_MAX);
+  for (int64_t lo = 0; lo < n; lo += span) {
+    const int64_t hi = std::min(n, lo + span);
+    if (int r = sort_by_label(labels, lo, hi, k, v, st)) return r;
+    const unsigned nb =
+        (unsigned)std::max<int64_t>(1, (hi - lo + CSR_SEGP - 1) / CSR_SEGP);
+    k_csr_seg_sums<<<dim3(nb, ny), CSR_SUMB, (size_t)td * 8, st>>>(
+        indptr, indices, data, v.sitems, v.soff, k, d, td, acc);
+    if (int r = check_launch("csr sums")) return r;
+  }
+  return 0;
+}
+
+static int csr_run(const int64_t *indptr, const int32_t *indices,
+                   const double *data, int64_t n, int64_t d, const double *C,
+                   int64_t k, const void *ws, size_t wsb, int32_t *labels,
+                   double *acc, int op, void *stream, const char *who) {
   if (n < 0 || d <= 0 || k <= 0 || d > INT32_MAX || k > INT32_MAX)
     return fail(DKM_E_ARG, std::string(who) + ": bad n/d/k");
   if (n == 0) return 0;
   if (!indptr || !C || (!indices && !data))
     return fail(DKM_E_ARG, std::string(who) + ": NULL input");
-  (void)C;  // the kernel reads C^T and |c|^2 prepared in the workspace
+  (void)C;  // the kernels read C^T and |c|^2 prepared in the workspace
   WsView v;
   if (int r = ws_view(ws, wsb, k, d, &v)) return r;
-  int dev = 0, cus = 256;
-  hipDeviceProp_t p;
-  if (hipGetDevice(&dev) == hipSuccess &&
-      hipGetDeviceProperties(&p, dev) == hipSuccess)
-    cus = p.multiProcessorCount;
-  const int64_t blocks = std::min<int64_t>((n + 3) / 4, (int64_t)cus * 16);
-  const unsigned g = (unsigned)std::max<int64_t>(1, blocks);
-  hipStream_t s = (hipStream_t)stream;
-#define DKM_CSR_R(KPL)                                                       \
-  k_csr_assign_r<KPL><<<g, 256, 0, s>>>(indptr, indices, data, n, (int)d,     \
-                                        v.ct64, v.cn64, (int)k, labels, acc)
-  if (DKM_AB_CSR_OLD || k > 512)
-    k_csr_assign<<<g, 256, 0, s>>>(indptr, indices, data, n, (int)d, v.ct64,
-                                   v.cn64, (int)k, labels, acc);
-  else if (k <= 64)
-    DKM_CSR_R(1);
-  else if (k <= 128)
-    DKM_CSR_R(2);
-  else if (k <= 256)
-    DKM_CSR_R(4);
-  else
-    DKM_CSR_R(8);
-#undef DKM_CSR_R
-  return check_launch(who);
+  if (op == OP_FULL && (!labels || !sorted_sums_ok(k, 1, v)))
+    op = OP_FULL_ATOMIC;  // no label array to sort (or k beyond the sort)
+  const int S = csr_slices(k, d);
+  const int ks = (int)round_up((k + S - 1) / S, CSR_PASS);
+  // per chunk sample: S slice states (20 B), x.x bound (4 B), list slot (4 B)
+  const int64_t chunk =
+      std::min<int64_t>(n, v.nq * 12 / (20 * S + 8));
+  if (chunk <= 0)
+    return fail(DKM_E_WORKSPACE, std::string(who) + ": workspace too small");
+  char *tail = (char *)v.queue;
+  SliceState *pst = (SliceState *)tail;
+  int32_t *pidx = (int32_t *)(pst + (int64_t)S * chunk);
+  float *pxx = (float *)(pidx + (int64_t)S * chunk);
+  int32_t *list = (int32_t *)(pxx + chunk);
+  uint32_t *nlist = &v.hdr->csr_nund;
+  hipStream_t st = (hipStream_t)stream;
+  const int cu = csr_cus();
+  const int npass = (ks + CSR_PASS - 1) / CSR_PASS;
+  for (int64_t i0 = 0; i0 < n; i0 += chunk) {
+    const int64_t m = std::min(chunk, n - i0);
+    const int64_t groups = (m + CSR_SPW - 1) / CSR_SPW;
+    const int64_t per_slice = std::max<int64_t>(
+        1, std::min<int64_t>((int64_t)cu * 8 / S,
+                             (groups + CSR_BLOCK / 64 - 1) / (CSR_BLOCK / 64)));
+    const unsigned g = (unsigned)(per_slice * S);
+#define DKM_SCREEN(NP)                                                       \
+  k_csr_screen<NP><<<g, CSR_BLOCK, 0, st>>>(indptr, indices, data, i0, m,   \
+                                            v.ct32, ct_ld(k), v.cn32,       \
+                                            (int)k, S, ks, pst, pidx, pxx)
+    if (npass >= 2)
+      DKM_SCREEN(2);
+    else
+      DKM_SCREEN(1);
+#undef DKM_SCREEN
+    if (hipMemsetAsync(nlist, 0, 4, st) != hipSuccess)
+      return fail(DKM_E_LAUNCH, std::string(who) + ": memset");
+    const unsigned gm = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>((m + 255) / 256, (int64_t)cu * 16));
+    k_csr_merge<<<gm, 256, 0, st>>>(indptr, indices, data, i0, m, (int)d,
+                                    (int)k, S, pst, pidx, pxx, labels, acc,
+                                    op, list, nlist);
+    k_csr_resolve<<<(unsigned)cu * 4, 256, 0, st>>>(
+        indptr, indices, data, i0, (int)d, v.ct64, ct_ld(k), v.cn64, (int)k,
+        labels, acc, op, list, nlist,
+        (unsigned long long *)&v.hdr->rechecked_total);
+    if (int r = check_launch(who)) return r;
+  }
+  if (op == OP_FULL)
+    return csr_full_sums(indptr, indices, data, n, (int)d, (int)k, labels,
+                         acc, v, st);
+  return 0;
 }
 
 }  // namespace dkm
@@ -196,8 +518,19 @@ int dkm_partial_sum_csr_f64(const int64_t *indptr, const int32_t *indices,
                             size_t ws_bytes, int32_t *labels, double *acc,
                             void *stream) {
   if (!acc) return fail(DKM_E_ARG, "partial_sum_csr: acc is NULL");
-  return csr_assign(indptr, indices, data, n, d, C, k, ws, ws_bytes, labels,
-                    acc, stream, "dkm_partial_sum_csr_f64");
+  return csr_run(indptr, indices, data, n, d, C, k, ws, ws_bytes, labels, acc,
+                 OP_FULL, stream, "dkm_partial_sum_csr_f64");
+}
+
+int dkm_assign_delta_csr_f64(const int64_t *indptr, const int32_t *indices,
+                             const double *data, int64_t n, int64_t d,
+                             const double *C, int64_t k, const void *ws,
+                             size_t ws_bytes, int32_t *labels, double *delta,
+                             void *stream) {
+  if (!labels || !delta)
+    return fail(DKM_E_ARG, "assign_delta_csr: labels/delta is NULL");
+  return csr_run(indptr, indices, data, n, d, C, k, ws, ws_bytes, labels,
+                 delta, OP_DELTA, stream, "dkm_assign_delta_csr_f64");
 }
 
 int dkm_predict_csr_f64(const int64_t *indptr, const int32_t *indices,
@@ -205,8 +538,8 @@ int dkm_predict_csr_f64(const int64_t *indptr, const int32_t *indices,
                         const double *C, int64_t k, const void *ws,
                         size_t ws_bytes, int32_t *labels, void *stream) {
   if (!labels) return fail(DKM_E_ARG, "predict_csr: labels is NULL");
-  return csr_assign(indptr, indices, data, n, d, C, k, ws, ws_bytes, labels,
-                    nullptr, stream, "dkm_predict_csr_f64");
+  return csr_run(indptr, indices, data, n, d, C, k, ws, ws_bytes, labels,
+                 nullptr, OP_PREDICT, stream, "dkm_predict_csr_f64");
 }
 
 }  // extern "C"

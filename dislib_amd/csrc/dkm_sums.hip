@@ -296,14 +296,23 @@ static int launch_seg(const TX *X, int64_t ldx, int d, const int32_t *sorted,
   return check_launch("segmented sums");
 }
 
-// Sort the items (explicit list of *ndev <= nh entries, or [lo, lo + nh))
-// by key, then add sign * row to acc[key] for each; keys outside [0, k)
-// (the previous label -1 of a first assignment) are dropped.
-template <class TX>
-static int sort_and_sum(const TX *X, int64_t ldx, int d, const int32_t *key,
-                        const int32_t *items, const int32_t *ndev, int64_t nh,
-                        int64_t lo, int k, double sign, double *acc,
-                        const WsView &v, hipStream_t s) {
+static int set_sort_lds() {
+  if (hipFuncSetAttribute((const void *)k_sort_scatter,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          SORT_KMAX * 8) != hipSuccess ||
+      hipFuncSetAttribute((const void *)k_sort_count,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          SORT_KMAX * 4) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "sorted sums: LDS attribute");
+  return 0;
+}
+
+// Counting sort of the items (explicit list of *ndev <= nh entries, or
+// [lo, lo + nh)) by key into v.sitems, cluster c at [v.soff[c],
+// v.soff[c+1]); keys outside [0, k) (a previous label -1) are dropped.
+static int sort_items(const int32_t *key, const int32_t *items,
+                      const int32_t *ndev, int64_t nh, int64_t lo, int k,
+                      const WsView &v, hipStream_t s) {
   const unsigned nb = (unsigned)std::max<int64_t>(1, (nh + SRANGE - 1) / SRANGE);
   if (hipMemsetAsync(v.scnt, 0, (size_t)k * 4, s) != hipSuccess)
     return fail(DKM_E_LAUNCH, "sorted sums: memset");
@@ -312,7 +321,24 @@ static int sort_and_sum(const TX *X, int64_t ldx, int d, const int32_t *key,
   k_sort_scan<<<1, SBLK, 0, s>>>(v.scnt, k, v.soff, v.scur);
   k_sort_scatter<<<nb, SBLK, (size_t)k * 8, s>>>(key, items, ndev, nh, lo, k,
                                                  v.scur, v.sitems);
-  if (int r = check_launch("label sort")) return r;
+  return check_launch("label sort");
+}
+
+int sort_by_label(const int32_t *lab, int64_t lo, int64_t hi, int k,
+                  const WsView &v, hipStream_t s) {
+  if (!sorted_sums_ok(k, hi - lo, v))
+    return fail(DKM_E_WORKSPACE, "label sort: scratch too small");
+  if (int r = set_sort_lds()) return r;
+  return sort_items(lab, nullptr, nullptr, hi - lo, lo, k, v, s);
+}
+
+// Sort the items by key, then add sign * row to acc[key] for each.
+template <class TX>
+static int sort_and_sum(const TX *X, int64_t ldx, int d, const int32_t *key,
+                        const int32_t *items, const int32_t *ndev, int64_t nh,
+                        int64_t lo, int k, double sign, double *acc,
+                        const WsView &v, hipStream_t s) {
+  if (int r = sort_items(key, items, ndev, nh, lo, k, v, s)) return r;
   return launch_seg<TX>(X, ldx, d, v.sitems, nh, v.soff, k, sign, acc, s);
 }
 
@@ -324,13 +350,7 @@ int sorted_sums(const TX *X, int64_t lo, int64_t hi, int d, int64_t ldx,
   const int64_t n = hi - lo;
   if (!sorted_sums_ok(k, n, v))
     return fail(DKM_E_WORKSPACE, "sorted sums: scratch too small");
-  if (hipFuncSetAttribute((const void *)k_sort_scatter,
-                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                          SORT_KMAX * 8) != hipSuccess ||
-      hipFuncSetAttribute((const void *)k_sort_count,
-                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                          SORT_KMAX * 4) != hipSuccess)
-    return fail(DKM_E_LAUNCH, "sorted sums: LDS attribute");
+  if (int r = set_sort_lds()) return r;
   if (!prev)
     return sort_and_sum<TX>(X, ldx, d, lab, nullptr, nullptr, n, lo, k, 1.0,
                             acc, v, s);

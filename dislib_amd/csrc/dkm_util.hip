@@ -53,7 +53,8 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
   b += round_up(k * dpad * 4, 256);   // c32
   b += round_up(k * 4, 256);          // cn32
   b += round_up(k * 8, 256);          // cn64
-  b += round_up(k * d * 8, 256);      // ct64
+  b += round_up(ct_ld(k) * d * 8, 256);  // ct64 (d x ct_ld(k))
+  b += round_up(ct_ld(k) * d * 4, 256);  // ct32
   b += round_up(kpad16(k) * dpad32(d) * 4, 256);  // cfrag
   b += round_up(kpad16(k) * 4, 256);  // cnpad
   b += round_up(kpad16(k) * dpad32(d) * 4, 256);  // bfrag (hi + lo bf16)
@@ -85,7 +86,9 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   v->cn64 = (double *)p;
   p += round_up(k * 8, 256);
   v->ct64 = (double *)p;
-  p += round_up(k * d * 8, 256);
+  p += round_up(ct_ld(k) * d * 8, 256);
+  v->ct32 = (float *)p;
+  p += round_up(ct_ld(k) * d * 4, 256);
   v->cfrag = (float *)p;
   p += round_up(kpad16(k) * dpad32(d) * 4, 256);
   v->cnpad = (float *)p;
@@ -167,22 +170,37 @@ __global__ void k_ws_header(WsHeader *h, int64_t k, int64_t d, int64_t dpad,
 }
 
 // one 256-thread block per centre
+constexpr int SEQ_CHUNK = 2048;  // row values staged in LDS per sequential pass
 __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ C,
                                                  int64_t k, int64_t d,
                                                  int64_t dpad, int flags,
                                                  WsView v) {
+  __shared__ double srow[SEQ_CHUNK];
   const int64_t c = blockIdx.x;
   const double *row = C + c * d;
+  const int64_t ld = ct_ld(k);
   for (int64_t t = threadIdx.x; t < dpad; t += blockDim.x) {
     const double val = t < d ? row[t] : 0.0;
     v.c32[c * dpad + t] = (float)val;
-    if (t < d) v.ct64[t * k + c] = val;  // C^T: re-check and CSR kernels
+    if (t < d) {
+      v.ct64[t * ld + c] = val;  // C^T: re-check, CSR
+      v.ct32[t * ld + c] = (float)val;
+    }
+  }
+  // sequential over t: sklearn row_norms(squared=True) order
+  // (utils/sparsefuncs_fast.pyx:26-44); exact zeros change nothing.  The
+  // row goes through LDS in chunks so that the one summing lane reads it
+  // at LDS latency, not HBM latency.
+  double n2 = 0.0;
+  for (int64_t t0 = 0; t0 < d; t0 += SEQ_CHUNK) {
+    const int m = (int)(d - t0 < SEQ_CHUNK ? d - t0 : SEQ_CHUNK);
+    __syncthreads();
+    for (int t = threadIdx.x; t < m; t += blockDim.x) srow[t] = row[t0 + t];
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int t = 0; t < m; ++t) n2 = n2 + srow[t] * srow[t];
   }
   if (threadIdx.x == 0) {
-    // sequential over t: sklearn row_norms(squared=True) order
-    // (utils/sparsefuncs_fast.pyx:26-44); exact zeros change nothing.
-    double n2 = 0.0;
-    for (int64_t t = 0; t < d; ++t) n2 = n2 + row[t] * row[t];
     v.cn64[c] = n2;
     v.cn32[c] = (float)n2;
     const double nrm = sqrt(n2);
@@ -283,17 +301,28 @@ __global__ void __launch_bounds__(256) k_update(const double *__restrict__ acc,
   double ss = 0.0;
   if (mode == DKM_SUMS_RECIP) {
     // sparse criterion (sklearn euclidean_distances, sequential sums):
-    // computed from old and new rows before the new row is stored.
-    if (threadIdx.x == 0) {
-      double dot = 0.0, aa = 0.0, bb = 0.0;
-      const double inv = cnt != 0.0 ? 1.0 / cnt : 0.0;
-      for (int64_t t = 0; t < d; ++t) {
-        const double old = C[c * d + t];
-        const double nv = cnt != 0.0 ? acc[c * d + t] * inv : old;
-        dot = dot + nv * old;
-        aa = aa + nv * nv;
-        bb = bb + old * old;
+    // computed from old and new rows before the new row is stored; the
+    // rows go through LDS in chunks (one lane sums, at LDS latency).
+    __shared__ double sold[SEQ_CHUNK], snew[SEQ_CHUNK];
+    double dot = 0.0, aa = 0.0, bb = 0.0;
+    const double inv = cnt != 0.0 ? 1.0 / cnt : 0.0;
+    for (int64_t t0 = 0; t0 < d; t0 += SEQ_CHUNK) {
+      const int m = (int)(d - t0 < SEQ_CHUNK ? d - t0 : SEQ_CHUNK);
+      __syncthreads();
+      for (int t = threadIdx.x; t < m; t += blockDim.x) {
+        const double old = C[c * d + t0 + t];
+        sold[t] = old;
+        snew[t] = cnt != 0.0 ? acc[c * d + t0 + t] * inv : old;
       }
+      __syncthreads();
+      if (threadIdx.x == 0)
+        for (int t = 0; t < m; ++t) {
+          dot = dot + snew[t] * sold[t];
+          aa = aa + snew[t] * snew[t];
+          bb = bb + sold[t] * sold[t];
+        }
+    }
+    if (threadIdx.x == 0) {
       double dd = -2.0 * dot;
       dd = dd + aa;
       dd = dd + bb;
@@ -403,14 +432,14 @@ int dkm_prepare_centers(const double *C, int64_t k, int64_t d, int flags,
   const int64_t dpad = round_up(d, 4);
   k_ws_header<<<1, 64, 0, s>>>(v.hdr, k, d, dpad, v.nq);
   k_prepare<<<(unsigned)k, 256, 0, s>>>(C, k, d, dpad, flags, v);
-  {
+  if (!(flags & DKM_PREP_CSR)) {  // the dense screens' centre tiles
     const int64_t tot = (kpad16(k) / 16) * (dpad32(d) / 32) * 512;
     const int64_t g = std::max<int64_t>(1, std::min<int64_t>((tot + 255) / 256,
                                                             4096));
     k_frag<<<(unsigned)g, 256, 0, s>>>(C, k, d, v);
   }
   if (int r = check_launch("dkm_prepare_centers")) return r;
-  if (gemm_path(k, d))
+  if (gemm_path(k, d) && !(flags & DKM_PREP_CSR))
     if (int r = gemm_prepare(C, k, d, v, s)) return r;
   if (acc) {
     hipError_t e = hipMemsetAsync(acc, 0, (size_t)(k * (d + 1)) * 8, s);

@@ -67,8 +67,10 @@ const char *dkm_last_error(void);
 size_t dkm_workspace_bytes(int64_t k, int64_t d, int64_t n_queue);
 
 /* prepare flags */
-#define DKM_PREP_CSR 1 /* also build the transposed fp64 centres C^T (d x k)
-                          used by the CSR kernels                           */
+#define DKM_PREP_CSR 1 /* prepare for the CSR kernels only: the transposed
+                          centres C^T (fp64 and fp32, d rows, stride k
+                          rounded up to 16) and |c|^2, without the dense
+                          screens' centre tiles                            */
 
 /* Derive per-iteration centre data (fp32 copy, |c|^2 in sklearn's sequential
  * order, error-bound scalars, optionally C^T) into the workspace and ZERO the
@@ -145,6 +147,14 @@ int dkm_partial_sum_csr_f64(const int64_t *indptr, const int32_t *indices,
                             const double *C, int64_t k, const void *ws,
                             size_t ws_bytes, int32_t *labels, double *acc,
                             void *stream);
+/* Incremental CSR form (the fit loop), same contract as
+ * dkm_assign_delta_f64: labels in/out (-1 = none), delta += the rows whose
+ * label changed (+x to the new cluster, -x from the previous one).       */
+int dkm_assign_delta_csr_f64(const int64_t *indptr, const int32_t *indices,
+                             const double *data, int64_t n, int64_t d,
+                             const double *C, int64_t k, const void *ws,
+                             size_t ws_bytes, int32_t *labels, double *delta,
+                             void *stream);
 int dkm_predict_csr_f64(const int64_t *indptr, const int32_t *indices,
                         const double *data, int64_t n, int64_t d,
                         const double *C, int64_t k, const void *ws,

@@ -219,42 +219,76 @@ def test_f07_sparse_csr():
     _close(km2.centers, g["dense_centers"], RTOL64)
 
 
-@pytest.mark.parametrize("n,d,k,per_row,seed", [
-    (2000, 400, 200, 90, 0),    # > 64 stored entries per row, 4 centres/lane
-    (3000, 5000, 256, 10, 1),   # C5 shape (scaled): 10 nnz/row, k = 256
-    (1500, 300, 60, 5, 2),      # 1 centre per lane
-    (1000, 200, 600, 20, 3)])   # k > 512: the per-centre-group kernel
-def test_csr_predict_and_partial_sum_vs_oracle(n, d, k, per_row, seed):
-    """CSR assignment (k_csr_assign_r / k_csr_assign) against the oracle's
-    sklearn-order arithmetic: labels bit-exact, sums 1e-12."""
+def _ragged_csr(rng, n, d, per_row):
+    """CSR rows with 0 .. 2*per_row sorted distinct columns (empty rows and
+    rows longer than one 16-entry staging chunk included)."""
+    counts = rng.integers(0, 2 * per_row + 1, n)
+    counts[::97] = 0
+    counts[5::89] = min(d, 40)
+    cols = [np.sort(rng.choice(d, c, replace=False)) for c in counts]
+    indptr = np.concatenate([[0], np.cumsum(counts)])
+    idx = np.concatenate(cols).astype(np.int32) if n else \
+        np.zeros(0, np.int32)
+    return sp.csr_matrix((rng.random(len(idx)), idx, indptr), shape=(n, d))
+
+
+@pytest.mark.parametrize("n,d,k,per_row,seed,nq", [
+    (2000, 400, 200, 90, 0, 0),     # > 16 stored entries: several chunks
+    (3000, 5000, 256, 10, 1, 0),    # 10 MB C^T: 4 centre slices
+    (1500, 300, 60, 5, 2, 0),       # one slice, one pass
+    (1000, 200, 600, 20, 3, 0),     # one slice, two 32-centre passes/walk
+    (2500, 10000, 256, 10, 4, 0),   # C5's d and k: 8 slices of 32 centres
+    (2100, 4000, 333, 8, 5, 0),     # odd k: uneven last slice, padded C^T
+    (1800, 10000, 256, 6, 6, 512)])  # small workspace tail: 50 sample chunks
+def test_csr_predict_and_partial_sum_vs_oracle(n, d, k, per_row, seed, nq):
+    """CSR assignment (k_csr_slice + k_csr_merge) against the oracle's
+    sklearn-order arithmetic on ragged rows: labels bit-exact, sums 1e-12;
+    then the incremental form from a perturbed previous assignment."""
     from dislib_amd import _device, _lib
     rng = np.random.default_rng(seed)
-    gap = max(1, d // per_row - 1)
-    cols = np.cumsum(rng.integers(1, gap + 1, (n, per_row)), axis=1) - 1
-    indptr = np.arange(0, n * per_row + 1, per_row)
-    xs = sp.csr_matrix((rng.random(n * per_row),
-                        cols.reshape(-1).astype(np.int32), indptr),
-                       shape=(n, d))
+    xs = _ragged_csr(rng, n, d, per_row)
     C = xs[rng.choice(n, k, replace=False)].toarray() + \
         rng.random((k, d)) * 0.05
     rl, rs, rc = orc.partial_sum(xs, sp.csr_matrix(C), sparse=True)
+    rs = np.asarray(rs.todense()) if sp.issparse(rs) else rs
     dev = torch.device("cuda")
     ds = _load(xs, n)
     dd = ds._device_data()
     Ct = torch.from_numpy(C).to(dev)
-    ws = _device.Workspace(k, d, dd.n, dev)
+    ws = _device.Workspace(k, d, nq or dd.n, dev)
     acc = torch.empty(k * (d + 1), dtype=torch.float64, device=dev)
     lab = torch.empty(dd.n, dtype=torch.int32, device=dev)
     _device.prepare(Ct, ws, acc, csr=True)
     _device.partial_sum(dd, Ct, ws, lab, acc, _lib.MODE_AUTO)
     assert np.array_equal(lab.cpu().numpy(), rl)
     a = acc.cpu().numpy()
-    _close(a[:k * d].reshape(k, d), np.asarray(rs.todense())
-           if sp.issparse(rs) else rs, 1e-12)
+    _close(a[:k * d].reshape(k, d), rs, 1e-12)
     assert np.array_equal(a[k * d:], np.asarray(rc, dtype=np.float64))
     lab2 = torch.full((dd.n,), -7, dtype=torch.int32, device=dev)
     _device.predict(dd, Ct, ws, lab2, _lib.MODE_AUTO)
     assert np.array_equal(lab2.cpu().numpy(), rl)
+    # delta: previous labels = the true ones with every 7th changed (and
+    # some -1 = never assigned); delta must move exactly those rows
+    prev = rl.copy()
+    prev[::7] = (prev[::7] + 1) % k
+    prev[3::11] = -1
+    lab3 = torch.from_numpy(prev.astype(np.int32)).to(dev)
+    _device.prepare(Ct, ws, acc, csr=True)
+    _device.assign_delta(dd, Ct, ws, lab3, acc, _lib.MODE_AUTO)
+    assert np.array_equal(lab3.cpu().numpy(), rl)
+    moved = prev != rl
+    want = np.zeros((k, d + 1))
+    xd = xs.toarray()
+    for i in np.nonzero(moved)[0]:
+        want[rl[i], :d] += xd[i]
+        want[rl[i], d] += 1
+        if prev[i] >= 0:
+            want[prev[i], :d] -= xd[i]
+            want[prev[i], d] -= 1
+    got = acc.cpu().numpy()
+    np.testing.assert_allclose(got[:k * d].reshape(k, d), want[:, :d],
+                               rtol=0, atol=1e-12)
+    assert np.array_equal(got[k * d:], want[:, d])
 
 
 # ---------------------------------------------------------------------------

@@ -53,6 +53,22 @@ def main():
         st.flag.item()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    # one full (refresh) assignment + sums, and predict, timed alone
+    from dislib_amd import _device, _lib
+    t0 = time.perf_counter()
+    st.prepare()
+    _device.partial_sum(st.dd, st.C, st.ws, st.labels, st.acc,
+                        _lib.MODE_AUTO)
+    torch.cuda.synchronize()
+    full_ms = (time.perf_counter() - t0) * 1e3
+    lab = torch.empty(st.dd.n, dtype=torch.int32, device=dev)
+    _device.predict(st.dd, st.C, st.ws, lab, _lib.MODE_AUTO)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        _device.predict(st.dd, st.C, st.ws, lab, _lib.MODE_AUTO)
+    torch.cuda.synchronize()
+    pred_ms = (time.perf_counter() - t0) / a.steps * 1e3
     nnz = a.n * a.nnz
     out = {"metric": "KMeans samples·iters/sec (sparse CSR fit)",
            "value": a.n * a.steps / el, "unit": "samples·iters/s",
@@ -60,7 +76,12 @@ def main():
            "config": {"workload": "CSR %dx%d, %d nnz/row, k=%d" %
                       (a.n, a.d, a.nnz, a.k), "nnz": nnz},
            "bytes_per_step": 12 * nnz + 8 * (a.n + 1),
-           "hbm_gbs": (12 * nnz + 8 * (a.n + 1)) / (el / a.steps) / 1e9}
+           "hbm_gbs": (12 * nnz + 8 * (a.n + 1)) / (el / a.steps) / 1e9,
+           "gather_bytes_per_step": 8 * nnz * a.k,
+           "gather_tbs": 8 * nnz * a.k / (el / a.steps) / 1e12,
+           "full_sums_iteration_ms": full_ms,
+           "predict_ms": pred_ms,
+           "predict_samples_per_s": a.n / (pred_ms * 1e-3)}
     print(json.dumps(out))
 
 
