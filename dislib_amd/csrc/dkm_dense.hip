@@ -1596,9 +1596,16 @@ __global__ void __launch_bounds__(SBB)
   if (lane == 0 && tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
 }
 
-// Two-candidate samples of k_screen_b1: lane per entry, the reference
-// arithmetic (numpy pairwise order, correctly rounded sqrt) on c1 and c2,
-// first index among equal distances.  Labels only.
+// Two-candidate samples of k_screen_b1: the reference arithmetic (numpy
+// pairwise order, correctly rounded sqrt) on c1 and c2, first index among
+// equal distances.  Labels only.  k_screen_b1 runs only for 8 <= d <= 128
+// with d % 8 == 0, where numpy's sum is one pairwise leaf: 8 accumulators
+// r_j = sum_i f(j + 8 i) combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)).
+// Lane (e, c, j) = (lane >> 4, (lane >> 3) & 1, lane & 7) keeps r_j of
+// candidate c of entry e, so the 8 lanes of a candidate read 64 contiguous
+// bytes per step (a lane-per-entry walk read one 8-B word per lane from 64
+// scattered rows); the combine tree is three xor shuffles (IEEE addition is
+// commutative, so both partners of a pair hold the same bits).
 template <class TX>
 __global__ void __launch_bounds__(BLOCK)
     k_cand2(const TX *__restrict__ X, int d, int64_t ldx,
@@ -1607,6 +1614,8 @@ __global__ void __launch_bounds__(BLOCK)
   const int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
   const int64_t nwv = (int64_t)gridDim.x * (BLOCK / 64);
   const int lane = threadIdx.x & 63;
+  const int e = lane >> 4, cs = (lane >> 3) & 1, j = lane & 7;
+  const int nst = d >> 3;
   unsigned long long mine = 0;
   // (segment, 64-entry batch) pairs over all waves, batch index major
   for (int64_t L = wv; L < (int64_t)nseg * (B1_CAP / 64); L += nwv) {
@@ -1614,14 +1623,29 @@ __global__ void __launch_bounds__(BLOCK)
     const int t0 = (int)(L / nseg) * 64;
     const int cnt = v.ccount[sg];
     if (t0 == 0 && lane == 0) mine += cnt;
-    if (t0 + lane >= cnt) continue;
-    const int2 it = v.clist[sg * B1_CAP + t0 + lane];
-    const int64_t si = base + it.x;
-    const int c1 = it.y & 0xffff, c2 = (int)((unsigned)it.y >> 16);
-    const TX *xr = X + si * ldx;
-    const double d1 = sqrt(pw_sum(SqDiff<TX>{xr, C + (int64_t)c1 * d}, d));
-    const double d2 = sqrt(pw_sum(SqDiff<TX>{xr, C + (int64_t)c2 * d}, d));
-    lab_out[si] = (d2 < d1 || (d2 == d1 && c2 < c1)) ? c2 : c1;
+    if (t0 >= cnt) continue;  // wave-uniform
+    const int2 *list = v.clist + sg * B1_CAP + t0;
+    const int m = min(64, cnt - t0);
+    for (int p = 0; p < m; p += 4) {
+      const bool live = p + e < m;
+      const int2 it = list[live ? p + e : 0];
+      const int c1 = it.y & 0xffff, c2 = (int)((unsigned)it.y >> 16);
+      const int64_t si = base + it.x;
+      const TX *xr = X + si * ldx + j;
+      const double *cr = C + (int64_t)(cs ? c2 : c1) * d + j;
+      double r = 0.0;
+      for (int i = 0; i < nst; ++i) {
+        const double df = (double)xr[8 * i] - cr[8 * i];
+        r = i ? r + df * df : df * df;
+      }
+      r = r + __shfl_xor(r, 1, 64);
+      r = r + __shfl_xor(r, 2, 64);
+      r = r + __shfl_xor(r, 4, 64);
+      const double dist = sqrt(r);
+      const double o = __shfl_xor(dist, 8, 64);  // the other candidate
+      if (live && cs == 0 && j == 0)
+        lab_out[si] = (o < dist || (o == dist && c2 < c1)) ? c2 : c1;
+    }
   }
   if (mine) atomicAdd((unsigned long long *)&v.hdr->rechecked_total, mine);
 }
