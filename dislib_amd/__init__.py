@@ -16,16 +16,19 @@ from dislib_amd._shard import shard_dataset, shard_range  # noqa: E402,F401
 
 
 def install_as_dislib():
-    """Alias ``dislib``, ``dislib.cluster`` and ``dislib.data`` to this
-    package (only the k-means path and its data containers)."""
+    """Alias ``dislib``, ``dislib.cluster``, ``dislib.data`` and
+    ``dislib.neighbors`` to this package (the k-means path, its data
+    containers and the kNN reuse of its distance primitive)."""
     import types
-    from dislib_amd import cluster, data
+    from dislib_amd import cluster, data, neighbors
     pkg = types.ModuleType("dislib")
     pkg.__path__ = []
     pkg.name = "dislib"
     pkg.cluster = cluster
     pkg.data = data
+    pkg.neighbors = neighbors
     sys.modules["dislib"] = pkg
+    sys.modules["dislib.neighbors"] = neighbors
     sys.modules["dislib.cluster"] = cluster
     sys.modules["dislib.data"] = data
     return pkg

@@ -54,6 +54,15 @@ SIGNATURES = {
     "dkm_make_blobs_f64": (_i32, [_p, _i64, _i64, _i64, _i64, _u64, _f64,
                                   _f64, _p, _p]),
     "dkm_screen_stats": (_i32, [_p, ctypes.POINTER(_i64), _p]),
+    # distance-primitive reuse (kNN, DBSCAN epsilon query)
+    "dkm_knn_workspace_bytes": (_sz, [_i64, _i64, _i64]),
+    "dkm_knn_f64": (_i32, [_p, _i64, _i64, _p, _i64, _i64, _i64, _i64, _p,
+                           _sz, _p, _p, _p]),
+    "dkm_radius_count_f64": (_i32, [_p, _i64, _i64, _p, _i64, _i64, _i64,
+                                    _f64, _p, _p]),
+    "dkm_radius_workspace_bytes": (_sz, [_i64, _i64]),
+    "dkm_radius_fill_f64": (_i32, [_p, _i64, _i64, _p, _i64, _i64, _i64,
+                                   _f64, _p, _p, _sz, _p, _p, _p]),
     # multi-GPU all-reduce (RCCL)
     "dkm_allreduce_unique_id": (_i32, [_p]),
     "dkm_allreduce_init_rank": (_i32, [ctypes.c_char_p, _i32, _i32, _i32]),

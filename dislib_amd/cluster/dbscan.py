@@ -1,0 +1,91 @@
+"""DBSCAN's epsilon query on the GPU distance primitive.
+
+Reference: ``_compute_neighbours`` of
+``/root/reference/dislib/cluster/dbscan/classes.py:124-141`` -- for every
+sample of rows ``[begin_idx, end_idx)`` of the concatenated Subsets, the
+indices of all samples whose ``_vec_matrix_euclid`` distance (``:153-154``,
+numpy's ``sqrt(add.reduce((x - s)**2))`` in its pairwise order) is below
+``epsilon``, ordered by distance, and whether there are at least
+``min_samples`` of them.  The rest of DBSCAN (grid regions, equivalence
+merging) is out of scope.
+
+Here the concatenated samples are uploaded once and ``dkm_radius_count_f64``
+/ ``dkm_radius_fill_f64`` compute the same fp64 distances (bit-exact: the
+k-means exact arithmetic), select ``dist < epsilon``, and sort each list by
+(distance, index).  The reference's ``np.argsort`` gives the same order
+except among exactly equal distances, which it may order differently.
+Dense Subsets only.
+"""
+import ctypes
+
+import numpy as np
+
+from .. import _lib
+from .._device import _is_torch, on, ptr, resolve, stream_ptr, torch
+
+
+def compute_neighbours(epsilon, min_samples, sparse, begin_idx, end_idx,
+                       *subsets, device=None):
+    """Same arguments and results as the reference task: a list of int64
+    index arrays (one per query sample) and a list of core-point flags."""
+    if sparse:
+        raise ValueError("compute_neighbours: sparse Subsets are not "
+                         "supported by the GPU path")
+    t = torch()
+    dev = resolve(device)
+    with on(dev):
+        X = _concat(subsets, dev)
+        n, d = X.shape
+        b, e = _slice_bounds(begin_idx, end_idx, n)
+        Q = X[b:e]
+        nq = e - b
+        if nq == 0:
+            return [], []
+        so = _lib.lib()
+        counts = t.empty(nq, dtype=t.int64, device=dev)
+        _lib.check(so.dkm_radius_count_f64(
+            ptr(Q), nq, X.stride(0), ptr(X), n, X.stride(0), d,
+            float(epsilon), ptr(counts), stream_ptr()), "dkm_radius_count")
+        c = counts.cpu().numpy()
+        offsets = np.concatenate([[0], np.cumsum(c)]).astype(np.int64)
+        total = int(offsets[-1])
+        off_d = t.from_numpy(offsets).to(dev)
+        out_i = t.empty(max(total, 1), dtype=t.int64, device=dev)
+        out_d = t.empty(max(total, 1), dtype=t.float64, device=dev)
+        wsb = int(so.dkm_radius_workspace_bytes(nq, total))
+        ws = t.empty(wsb, dtype=t.uint8, device=dev)
+        _lib.check(so.dkm_radius_fill_f64(
+            ptr(Q), nq, X.stride(0), ptr(X), n, X.stride(0), d,
+            float(epsilon), ptr(off_d), ctypes.c_void_p(ws.data_ptr()), wsb,
+            ptr(out_i), ptr(out_d), stream_ptr()), "dkm_radius_fill")
+        idx = out_i[:total].cpu().numpy()
+    neigh = [idx[offsets[i]:offsets[i + 1]] for i in range(nq)]
+    core = [bool(c[i] >= min_samples) for i in range(nq)]
+    return neigh, core
+
+
+def _concat(subsets, dev):
+    """The concatenated samples as one fp64 (n, d) device matrix
+    (``_concatenate_subsets``, classes.py:144-150)."""
+    t = torch()
+    if not subsets:
+        raise ValueError("compute_neighbours: no Subsets")
+    parts = []
+    for s in subsets:
+        x = s.samples
+        if _is_torch(x):
+            parts.append(x.to(dev, dtype=t.float64))
+        else:
+            if hasattr(x, "toarray"):
+                raise ValueError("compute_neighbours: sparse Subsets are not"
+                                 " supported by the GPU path")
+            parts.append(t.from_numpy(np.ascontiguousarray(
+                np.asarray(x, dtype=np.float64))).to(dev))
+    X = parts[0] if len(parts) == 1 else t.cat(parts, 0)
+    return X.contiguous()
+
+
+def _slice_bounds(begin, end, n):
+    """``samples[begin:end]`` bounds with Python slice semantics."""
+    b, e, _ = slice(begin, end).indices(n)
+    return b, max(b, e)

@@ -1,0 +1,511 @@
+// dkm_neighbors.hip -- the distance primitive reused outside the Lloyd loop
+// (SURVEY.md 8 f4).
+//
+// * kNN: NearestNeighbors.kneighbors (reference neighbors/base.py:40-87).
+//   The reference fits sklearn NearestNeighbors on every fit Subset, queries
+//   it with every query Subset and merges the per-pair k-lists by sort.
+//   sklearn's kd_tree (its choice for d <= 15) ranks by the sequential
+//   squared sum  r = 0; r += (q_t - x_t)^2  (EuclideanDistance.rdist, no
+//   FMA) and reports sqrt(r).  Here one brute-force pass over the whole fit
+//   set computes that same r for every (query, fit row) pair and keeps the
+//   k smallest by (r, index):
+//     k_knn_part   lane = query (its row in VGPRs), wave-uniform fit row j
+//                  read by scalar loads (constant address space: SGPRs, no
+//                  LDS broadcast), fit rows cut into P partitions so that
+//                  (queries / 64) x P waves fill the chip; a per-lane sorted
+//                  top-K (K = 1..32, registers, unrolled insertion network
+//                  entered only by lanes whose r beats their K-th).
+//     k_knn_merge  lane = query: the P partial lists merged by (r, index),
+//                  sqrt, int64 indices.
+//   Roofline: VALU fp64 -- 3 d ops (sub, mul, add) per pair.
+//
+// * Epsilon query: DBSCAN _compute_neighbours (reference
+//   cluster/dbscan/classes.py:124-141): for each query row, every row with
+//   _vec_matrix_euclid distance < eps (numpy's pairwise order, the k-means
+//   exact arithmetic of dkm_internal.h), sorted by distance.
+//     k_radius<PASS> lane = query, fit rows partitioned over waves; pass 0
+//                  counts (int64 atomics per lane-partition), pass 1 writes
+//                  (index, distance) at an atomically advanced cursor;
+//     k_seg_sort   block per query list: (distance, index) ascending --
+//                  bitonic in LDS up to 4096 entries, a rank sort through
+//                  workspace scratch beyond.
+#include "dkm_internal.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace dkm {
+
+namespace {
+
+constexpr int NB = 256;  // threads per block (4 waves)
+typedef const __attribute__((address_space(4))) double cdouble;
+
+// ---------------------------------------------------------------------------
+// kNN
+// ---------------------------------------------------------------------------
+template <int K>
+struct TopK {
+  double r[K];
+  int i[K];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      r[s] = INFINITY;
+      i[s] = INT32_MAX;
+    }
+  }
+  // (v, j) with j larger than every index already held (scan order), so a
+  // strict < keeps the earlier index first among equal r
+  __device__ __forceinline__ void push_seq(double v, int j) {
+    if (v < r[K - 1]) {
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        const bool lt = v < r[s];
+        const double tr = r[s];
+        const int ti = i[s];
+        r[s] = lt ? v : tr;
+        i[s] = lt ? j : ti;
+        v = lt ? tr : v;
+        j = lt ? ti : j;
+      }
+    }
+  }
+  // arbitrary (v, j): lexicographic (r, index)
+  __device__ __forceinline__ void push_lex(double v, int j) {
+    if (v < r[K - 1] || (v == r[K - 1] && j < i[K - 1])) {
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        const bool lt = v < r[s] || (v == r[s] && j < i[s]);
+        const double tr = r[s];
+        const int ti = i[s];
+        r[s] = lt ? v : tr;
+        i[s] = lt ? j : ti;
+        v = lt ? tr : v;
+        j = lt ? ti : j;
+      }
+    }
+  }
+};
+
+// Sequential squared distance of a register-resident query to fit row xr
+// (wave-uniform: scalar loads).  MAXD = 0: the query is read from global.
+template <int MAXD>
+__device__ __forceinline__ double seq_r(const double (&q)[MAXD > 0 ? MAXD : 1],
+                                        const double *qg, cdouble *xr, int d) {
+  double r = 0.0;
+  if constexpr (MAXD > 0) {
+#pragma unroll
+    for (int t = 0; t < MAXD; ++t)
+      if (t < d) {
+        const double df = q[t] - xr[t];
+        r = r + df * df;
+      }
+  } else {
+    for (int t = 0; t < d; ++t) {
+      const double df = qg[t] - xr[t];
+      r = r + df * df;
+    }
+  }
+  return r;
+}
+
+template <int MAXD, int K>
+__global__ void __launch_bounds__(NB)
+    k_knn_part(const double *__restrict__ Q, int64_t nq, int64_t ldq,
+               const double *__restrict__ X, int64_t nx, int64_t ldx, int d,
+               int64_t plen, int P, double *__restrict__ pr,
+               int *__restrict__ pi) {
+  const int lane = threadIdx.x & 63;
+  const int64_t qg = (int64_t)blockIdx.x * (NB / 64) +
+                     __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int p = blockIdx.y;
+  const int64_t q = qg * 64 + lane;
+  if (qg * 64 >= nq) return;  // wave-uniform
+  const bool live = q < nq;
+  const double *qrow = Q + (live ? q : 0) * ldq;
+  double qv[MAXD > 0 ? MAXD : 1];
+  if constexpr (MAXD > 0) {
+#pragma unroll
+    for (int t = 0; t < MAXD; ++t) qv[t] = t < d ? qrow[t] : 0.0;
+  }
+  TopK<K> top;
+  top.init();
+  const int64_t j0 = (int64_t)p * plen;
+  const int64_t j1 = std::min<int64_t>(nx, j0 + plen);
+  cdouble *xc = (cdouble *)X;
+  for (int64_t j = j0; j < j1; ++j) {
+    const double r = seq_r<MAXD>(qv, qrow, xc + j * ldx, d);
+    top.push_seq(r, (int)j);
+  }
+  if (!live) return;
+  double *po = pr + (q * P + p) * K;
+  int *io = pi + (q * P + p) * K;
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    po[s] = top.r[s];
+    io[s] = top.i[s];
+  }
+}
+
+template <int K>
+__global__ void __launch_bounds__(NB)
+    k_knn_merge(const double *__restrict__ pr, const int *__restrict__ pi,
+                int64_t nq, int P, int kn, double *__restrict__ out_d,
+                int64_t *__restrict__ out_i) {
+  const int64_t q = (int64_t)blockIdx.x * NB + threadIdx.x;
+  if (q >= nq) return;
+  TopK<K> top;
+  top.init();
+  for (int p = 0; p < P; ++p) {
+    const double *a = pr + (q * P + p) * K;
+    const int *b = pi + (q * P + p) * K;
+    for (int s = 0; s < kn; ++s) {
+      const double v = a[s];
+      if (!(v < top.r[K - 1]) && !(v == top.r[K - 1] && b[s] < top.i[K - 1]))
+        break;  // the partition's list is sorted: nothing further enters
+      top.push_lex(v, b[s]);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < K; ++s)
+    if (s < kn) {
+      out_d[q * kn + s] = sqrt(top.r[s]);
+      out_i[q * kn + s] = (int64_t)top.i[s];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// epsilon query
+// ---------------------------------------------------------------------------
+template <int MAXD, int PASS>
+__global__ void __launch_bounds__(NB)
+    k_radius(const double *__restrict__ Q, int64_t nq, int64_t ldq,
+             const double *__restrict__ X, int64_t nx, int64_t ldx, int d,
+             double eps, int64_t plen, unsigned long long *__restrict__ cnt,
+             int64_t *__restrict__ out_i, double *__restrict__ out_d) {
+  const int lane = threadIdx.x & 63;
+  const int64_t qg = (int64_t)blockIdx.x * (NB / 64) +
+                     __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int p = blockIdx.y;
+  const int64_t q = qg * 64 + lane;
+  if (qg * 64 >= nq) return;
+  const bool live = q < nq;
+  const double *qrow = Q + (live ? q : 0) * ldq;
+  double qv[MAXD > 0 ? MAXD : 8];
+  if constexpr (MAXD > 0) {
+#pragma unroll
+    for (int t = 0; t < MAXD; ++t) qv[t] = t < d ? qrow[t] : 0.0;
+  }
+  const int64_t j0 = (int64_t)p * plen;
+  const int64_t j1 = std::min<int64_t>(nx, j0 + plen);
+  cdouble *xc = (cdouble *)X;
+  unsigned long long mine = 0;
+  for (int64_t j = j0; j < j1; ++j) {
+    double r;
+    if constexpr (MAXD > 0)
+      r = exact_sqdist_reg<MAXD>(qv, xc + j * ldx, d);
+    else
+      r = pw_sum(SqDiff<double>{qrow, X + j * ldx}, d);
+    // _vec_matrix_euclid computes row - sample; (a - b)^2 == (b - a)^2
+    const double dist = sqrt(r);
+    if (live && dist < eps) {
+      if constexpr (PASS == 0) {
+        ++mine;
+      } else {
+        const unsigned long long at = atomicAdd(cnt + q, 1ull);
+        out_i[at] = j;
+        out_d[at] = dist;
+      }
+    }
+  }
+  if constexpr (PASS == 0)
+    if (live && mine) atomicAdd(cnt + q, mine);
+}
+
+constexpr int SORT_CAP = 4096;
+
+__device__ __forceinline__ bool key_lt(double da, int64_t ia, double db,
+                                       int64_t ib) {
+  return da < db || (da == db && ia < ib);
+}
+
+__global__ void __launch_bounds__(NB)
+    k_seg_sort(const int64_t *__restrict__ offsets, int64_t nq,
+               int64_t *__restrict__ idx, double *__restrict__ dist,
+               int64_t *__restrict__ sidx, double *__restrict__ sdist) {
+  __shared__ double sd[SORT_CAP];
+  __shared__ int64_t si[SORT_CAP];
+  const int64_t q = blockIdx.x;
+  if (q >= nq) return;
+  const int64_t o = offsets[q];
+  const int64_t m = offsets[q + 1] - o;
+  if (m <= 1) return;
+  if (m <= SORT_CAP) {
+    int p2 = 2;
+    while (p2 < m) p2 <<= 1;
+    for (int e = threadIdx.x; e < p2; e += NB) {
+      sd[e] = e < m ? dist[o + e] : INFINITY;
+      si[e] = e < m ? idx[o + e] : INT64_MAX;
+    }
+    __syncthreads();
+    for (int size = 2; size <= p2; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int e = threadIdx.x; e < p2; e += NB) {
+          const int f = e ^ stride;
+          if (f > e) {
+            const bool up = (e & size) == 0;
+            const bool gt = key_lt(sd[f], si[f], sd[e], si[e]);
+            if (gt == up) {
+              const double td = sd[e];
+              sd[e] = sd[f];
+              sd[f] = td;
+              const int64_t ti = si[e];
+              si[e] = si[f];
+              si[f] = ti;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (int e = threadIdx.x; e < m; e += NB) {
+      dist[o + e] = sd[e];
+      idx[o + e] = si[e];
+    }
+    return;
+  }
+  // beyond LDS: rank of each entry among the list (keys are distinct: the
+  // indices are), written to the scratch copy, then copied back
+  for (int64_t e = threadIdx.x; e < m; e += NB) {
+    const double de = dist[o + e];
+    const int64_t ie = idx[o + e];
+    int64_t rank = 0;
+    for (int64_t f = 0; f < m; ++f) rank += key_lt(dist[o + f], idx[o + f], de, ie);
+    sdist[o + rank] = de;
+    sidx[o + rank] = ie;
+  }
+  __syncthreads();
+  for (int64_t e = threadIdx.x; e < m; e += NB) {
+    dist[o + e] = sdist[o + e];
+    idx[o + e] = sidx[o + e];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+int knn_k(int64_t kn) {
+  int K = 1;
+  while (K < kn) K <<= 1;
+  return K;
+}
+
+int maxd_of(int64_t d) {
+  return d <= 8 ? 8 : d <= 16 ? 16 : d <= 32 ? 32 : d <= 64 ? 64 : 0;
+}
+
+// waves = groups x P >= 4096 (16 per CU of 256; a fixed target, so the
+// workspace size does not depend on the device); partitions no shorter than
+// 256 rows
+void knn_grid(int64_t nq, int64_t nx, int64_t *plen, int *P) {
+  const int64_t groups = (nq + 63) / 64;
+  const int64_t want = 4096;
+  int64_t p = std::max<int64_t>(1, (want + groups - 1) / groups);
+  p = std::min<int64_t>(p, std::max<int64_t>(1, nx / 256));
+  p = std::min<int64_t>(p, 65535);
+  *plen = (nx + p - 1) / p;
+  *P = (int)((nx + *plen - 1) / *plen);
+}
+
+template <int MAXD, int K>
+void launch_knn_part(dim3 g, hipStream_t s, const double *Q, int64_t nq,
+                     int64_t ldq, const double *X, int64_t nx, int64_t ldx,
+                     int d, int64_t plen, int P, double *pr, int *pi) {
+  k_knn_part<MAXD, K><<<g, NB, 0, s>>>(Q, nq, ldq, X, nx, ldx, d, plen, P, pr,
+                                       pi);
+}
+
+template <int K>
+int knn_dispatch(int maxd, dim3 g, hipStream_t s, const double *Q, int64_t nq,
+                 int64_t ldq, const double *X, int64_t nx, int64_t ldx, int d,
+                 int64_t plen, int P, double *pr, int *pi) {
+  switch (maxd) {
+    case 8: launch_knn_part<8, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi); break;
+    case 16: launch_knn_part<16, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi); break;
+    case 32: launch_knn_part<32, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi); break;
+    case 64: launch_knn_part<64, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi); break;
+    default: launch_knn_part<0, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi); break;
+  }
+  return check_launch("knn partial lists");
+}
+
+int knn_args(const double *Q, int64_t nq, int64_t ldq, const double *X,
+             int64_t nx, int64_t ldx, int64_t d, int64_t kn) {
+  if (nq < 0 || nx < 1 || d < 1 || ldq < d || ldx < d)
+    return fail(DKM_E_ARG, "knn: bad nq/nx/d/ld");
+  if (kn < 1 || kn > 32 || kn > nx)
+    return fail(DKM_E_ARG, "knn: n_neighbors must be in [1, min(32, nx)]");
+  if (nx > INT32_MAX || d > INT32_MAX)
+    return fail(DKM_E_ARG, "knn: nx/d too large");
+  if (nq > 0 && (!Q || !X)) return fail(DKM_E_ARG, "knn: NULL Q/X");
+  return 0;
+}
+
+template <int MAXD, int PASS>
+void launch_radius(dim3 g, hipStream_t s, const double *Q, int64_t nq,
+                   int64_t ldq, const double *X, int64_t nx, int64_t ldx,
+                   int d, double eps, int64_t plen, unsigned long long *cnt,
+                   int64_t *oi, double *od) {
+  k_radius<MAXD, PASS><<<g, NB, 0, s>>>(Q, nq, ldq, X, nx, ldx, d, eps, plen,
+                                        cnt, oi, od);
+}
+
+template <int PASS>
+int radius_dispatch(int64_t d, dim3 g, hipStream_t s, const double *Q,
+                    int64_t nq, int64_t ldq, const double *X, int64_t nx,
+                    int64_t ldx, double eps, int64_t plen,
+                    unsigned long long *cnt, int64_t *oi, double *od) {
+  const int di = (int)d;
+  // d <= 64: the query row in VGPRs (exact_sqdist_reg, one pairwise leaf)
+  const int maxd = maxd_of(d);
+  switch (maxd) {
+    case 8: launch_radius<8, PASS>(g, s, Q, nq, ldq, X, nx, ldx, di, eps, plen, cnt, oi, od); break;
+    case 16: launch_radius<16, PASS>(g, s, Q, nq, ldq, X, nx, ldx, di, eps, plen, cnt, oi, od); break;
+    case 32: launch_radius<32, PASS>(g, s, Q, nq, ldq, X, nx, ldx, di, eps, plen, cnt, oi, od); break;
+    case 64: launch_radius<64, PASS>(g, s, Q, nq, ldq, X, nx, ldx, di, eps, plen, cnt, oi, od); break;
+    default: launch_radius<0, PASS>(g, s, Q, nq, ldq, X, nx, ldx, di, eps, plen, cnt, oi, od); break;
+  }
+  return check_launch(PASS == 0 ? "radius count" : "radius fill");
+}
+
+int radius_args(const double *Q, int64_t nq, int64_t ldq, const double *X,
+                int64_t nx, int64_t ldx, int64_t d, double eps) {
+  if (nq < 0 || nx < 0 || d < 1 || ldq < d || ldx < d)
+    return fail(DKM_E_ARG, "radius: bad nq/nx/d/ld");
+  if (d > INT32_MAX) return fail(DKM_E_ARG, "radius: d too large");
+  if (std::isnan(eps)) return fail(DKM_E_ARG, "radius: eps is NaN");
+  if (nq > 0 && nx > 0 && (!Q || !X)) return fail(DKM_E_ARG, "radius: NULL Q/X");
+  return 0;
+}
+
+}  // namespace
+}  // namespace dkm
+
+using namespace dkm;
+
+extern "C" {
+
+size_t dkm_knn_workspace_bytes(int64_t nq, int64_t nx, int64_t kn) {
+  if (nq < 0 || nx < 1 || kn < 1 || kn > 32) return 0;
+  int64_t plen;
+  int P;
+  knn_grid(std::max<int64_t>(nq, 1), nx, &plen, &P);
+  const int K = knn_k(kn);
+  return (size_t)std::max<int64_t>(nq, 1) * P * K * (8 + 4) + 256;
+}
+
+int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
+                int64_t nx, int64_t ldx, int64_t d, int64_t kn, void *ws,
+                size_t ws_bytes, double *out_dist, int64_t *out_idx,
+                void *stream) {
+  if (int r = knn_args(Q, nq, ldq, X, nx, ldx, d, kn)) return r;
+  if (nq == 0) return 0;
+  if (!out_dist || !out_idx) return fail(DKM_E_ARG, "knn: NULL outputs");
+  const size_t need = dkm_knn_workspace_bytes(nq, nx, kn);
+  if (!ws || ws_bytes < need)
+    return fail(DKM_E_WORKSPACE, "knn: workspace smaller than "
+                                 "dkm_knn_workspace_bytes()");
+  hipStream_t s = (hipStream_t)stream;
+  int64_t plen;
+  int P;
+  knn_grid(nq, nx, &plen, &P);
+  const int K = knn_k(kn);
+  double *pr = (double *)ws;
+  int *pi = (int *)(pr + (size_t)nq * P * K);
+  const dim3 g((unsigned)((nq + 255) / 256), (unsigned)P);
+  const int maxd = maxd_of(d);
+  int r;
+  switch (K) {
+    case 1: r = knn_dispatch<1>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
+    case 2: r = knn_dispatch<2>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
+    case 4: r = knn_dispatch<4>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
+    case 8: r = knn_dispatch<8>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
+    case 16: r = knn_dispatch<16>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
+    default: r = knn_dispatch<32>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
+  }
+  if (r) return r;
+  const unsigned gm = (unsigned)((nq + NB - 1) / NB);
+  switch (K) {
+    case 1: k_knn_merge<1><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
+    case 2: k_knn_merge<2><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
+    case 4: k_knn_merge<4><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
+    case 8: k_knn_merge<8><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
+    case 16: k_knn_merge<16><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
+    default: k_knn_merge<32><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
+  }
+  return check_launch("knn merge");
+}
+
+int dkm_radius_count_f64(const double *Q, int64_t nq, int64_t ldq,
+                         const double *X, int64_t nx, int64_t ldx, int64_t d,
+                         double eps, int64_t *counts, void *stream) {
+  if (int r = radius_args(Q, nq, ldq, X, nx, ldx, d, eps)) return r;
+  if (nq == 0) return 0;
+  if (!counts) return fail(DKM_E_ARG, "radius: NULL counts");
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(counts, 0, (size_t)nq * 8, s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "radius: memset");
+  if (nx == 0) return 0;
+  int64_t plen;
+  int P;
+  knn_grid(nq, nx, &plen, &P);
+  const dim3 g((unsigned)((nq + 255) / 256), (unsigned)P);
+  return radius_dispatch<0>(d, g, s, Q, nq, ldq, X, nx, ldx, eps, plen,
+                            (unsigned long long *)counts, nullptr, nullptr);
+}
+
+size_t dkm_radius_workspace_bytes(int64_t nq, int64_t total) {
+  if (nq < 0 || total < 0) return 0;
+  return (size_t)nq * 8 + (size_t)total * 16 + 256;
+}
+
+int dkm_radius_fill_f64(const double *Q, int64_t nq, int64_t ldq,
+                        const double *X, int64_t nx, int64_t ldx, int64_t d,
+                        double eps, const int64_t *offsets, void *ws,
+                        size_t ws_bytes, int64_t *out_idx, double *out_dist,
+                        void *stream) {
+  if (int r = radius_args(Q, nq, ldq, X, nx, ldx, d, eps)) return r;
+  if (nq == 0 || nx == 0) return 0;
+  if (!offsets || !out_idx || !out_dist)
+    return fail(DKM_E_ARG, "radius: NULL offsets/outputs");
+  hipStream_t s = (hipStream_t)stream;
+  int64_t total = 0;
+  if (hipMemcpyAsync(&total, offsets + nq, 8, hipMemcpyDeviceToHost, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "radius: reading offsets[nq]");
+  if (total < 0) return fail(DKM_E_ARG, "radius: offsets[nq] < 0");
+  if (!ws || ws_bytes < dkm_radius_workspace_bytes(nq, total))
+    return fail(DKM_E_WORKSPACE, "radius: workspace smaller than "
+                                 "dkm_radius_workspace_bytes()");
+  // cursors = offsets[0..nq)
+  unsigned long long *cur = (unsigned long long *)ws;
+  int64_t *sidx = (int64_t *)((char *)ws + (size_t)nq * 8);
+  double *sdist = (double *)(sidx + total);
+  if (hipMemcpyAsync(cur, offsets, (size_t)nq * 8, hipMemcpyDeviceToDevice,
+                     s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "radius: cursor copy");
+  int64_t plen;
+  int P;
+  knn_grid(nq, nx, &plen, &P);
+  const dim3 g((unsigned)((nq + 255) / 256), (unsigned)P);
+  if (int r = radius_dispatch<1>(d, g, s, Q, nq, ldq, X, nx, ldx, eps, plen,
+                                 cur, out_idx, out_dist))
+    return r;
+  if (total == 0) return 0;
+  k_seg_sort<<<(unsigned)nq, NB, 0, s>>>(offsets, nq, out_idx, out_dist, sidx,
+                                         sdist);
+  return check_launch("radius sort");
+}
+
+}  // extern "C"

@@ -195,6 +195,45 @@ int dkm_make_blobs_f64(double *X, int64_t row0, int64_t n, int64_t d,
 int dkm_screen_stats(const void *ws, int64_t *n_rechecked, void *stream);
 
 /* ------------------------------------------------------------------------
+ * Distance-primitive reuse outside the Lloyd loop (SURVEY.md section 8
+ * row f4).  fp64 rows, row-major with leading dimensions; device pointers;
+ * stream-ordered.
+ * --------------------------------------------------------------------- */
+
+/* Workspace bytes of dkm_knn_f64 (0 for invalid sizes). */
+size_t dkm_knn_workspace_bytes(int64_t nq, int64_t nx, int64_t kn);
+/* For each query row of Q (nq x d): the kn (1..32, <= nx) rows of X
+ * (nx x d) nearest by dist = sqrt(r), r = sum_t (q_t - x_t)^2 summed
+ * sequentially from t = 0 (sklearn KD-tree EuclideanDistance.rdist, the
+ * regime sklearn picks for d <= 15), ascending (r, index).  out_dist
+ * nq x kn fp64, out_idx nq x kn int64 (row indices of X).
+ * Replaces NearestNeighbors.kneighbors: _get_neighbors per Subset pair and
+ * _merge_queries (dislib/neighbors/base.py:40-111). */
+int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
+                int64_t nx, int64_t ldx, int64_t d, int64_t kn, void *ws,
+                size_t ws_bytes, double *out_dist, int64_t *out_idx,
+                void *stream);
+
+/* DBSCAN epsilon query, replacing _compute_neighbours (dense) of
+ * dislib/cluster/dbscan/classes.py:124-141: for query row q, the rows j of
+ * X with numpy's sqrt(pairwise-sum((q - x_j)^2)) < eps (_vec_matrix_euclid,
+ * :153-154).  Step 1: counts[nq] (int64) <- neighbour counts. */
+int dkm_radius_count_f64(const double *Q, int64_t nq, int64_t ldq,
+                         const double *X, int64_t nx, int64_t ldx, int64_t d,
+                         double eps, int64_t *counts, void *stream);
+/* Workspace bytes of dkm_radius_fill_f64 for `total` neighbours. */
+size_t dkm_radius_workspace_bytes(int64_t nq, int64_t total);
+/* Step 2: offsets[nq+1] = exclusive prefix sum of the counts (device);
+ * list q goes to out_idx/out_dist[offsets[q] .. offsets[q+1]), ascending
+ * (distance, index).  Reads offsets[nq] to the host (synchronises
+ * `stream`). */
+int dkm_radius_fill_f64(const double *Q, int64_t nq, int64_t ldq,
+                        const double *X, int64_t nx, int64_t ldx, int64_t d,
+                        double eps, const int64_t *offsets, void *ws,
+                        size_t ws_bytes, int64_t *out_idx, double *out_dist,
+                        void *stream);
+
+/* ------------------------------------------------------------------------
  * Dataset loaders.  HOST functions: `buf`
  * and every output are host pointers; no GPU is touched.  `buf` holds
  * the whole file (len bytes); lines end at "\n", "\r\n" or "\r" (Python

@@ -1,0 +1,67 @@
+"""CPU: the f4 oracle (oracle/neighbors_oracle.py) against the golden vectors
+the reference itself wrote (tests/golden/gen_golden_neighbors.py):
+NearestNeighbors.kneighbors (neighbors/base.py:40-87) and the DBSCAN epsilon
+query _compute_neighbours (cluster/dbscan/classes.py:124-141)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import neighbors_oracle as orc
+
+G = np.load(os.path.join(os.path.dirname(__file__), "golden",
+                         "neighbors_ref.npz"))
+KNN = sorted({k.split("__")[0] for k in G.files if k.startswith("kn_")})
+DB = sorted({k.split("__")[0] for k in G.files if k.startswith("db_")})
+
+
+def _blocks(x, sub):
+    return [x[i:i + sub] for i in range(0, len(x), sub)]
+
+
+def knn_case(name):
+    sub, kn = (int(v) for v in G[name + "__meta"])
+    return (G[name + "__xf"], G[name + "__xq"], sub, kn,
+            G[name + "__dist"], G[name + "__ind"])
+
+
+def kd_tree_regime(xf, sub, kn):
+    return xf.shape[1] <= 15 and kn < sub // 2
+
+
+@pytest.mark.parametrize("name", KNN)
+def test_oracle_kneighbors_is_the_reference(name):
+    xf, xq, sub, kn, dist, ind = knn_case(name)
+    d, i = orc.kneighbors(_blocks(xf, sub), _blocks(xq, sub), kn)
+    assert np.array_equal(i, ind)
+    assert np.array_equal(d, dist)
+
+
+@pytest.mark.parametrize("name", KNN)
+def test_sequential_restatement(name):
+    """The GPU contract (one brute-force pass, sequential squared sums,
+    ascending (r, index)) against the reference: bit-exact in sklearn's
+    kd_tree regime, within the GEMM expansion's rounding otherwise."""
+    xf, xq, sub, kn, dist, ind = knn_case(name)
+    d, i = orc.kneighbors_exact(xf, xq, kn)
+    assert np.array_equal(i, ind), name
+    if kd_tree_regime(xf, sub, kn):
+        assert np.array_equal(d, dist), name
+    else:
+        # |x|^2 - 2 x.y + |y|^2 in fp64: error ~ eps (|x|^2 + |y|^2) on the
+        # squared distance (sqrt magnifies it near 0: compare squares)
+        scale2 = (xf ** 2).sum(1).max() + (xq ** 2).sum(1).max()
+        assert np.max(np.abs(d ** 2 - dist ** 2)) <= 1e-13 * scale2, name
+
+
+@pytest.mark.parametrize("name", DB)
+def test_oracle_epsilon_query_is_the_reference(name):
+    x = G[name + "__x"]
+    sub, eps, ms, b, e = G[name + "__meta"]
+    nl, cp = orc.compute_neighbours(eps, ms, int(b), int(e), x)
+    off = G[name + "__offsets"]
+    ref = G[name + "__neigh"]
+    assert len(nl) == len(off) - 1
+    for r, v in enumerate(nl):
+        assert np.array_equal(v, ref[off[r]:off[r + 1]]), (name, r)
+    assert np.array_equal(np.array(cp), G[name + "__core"])
