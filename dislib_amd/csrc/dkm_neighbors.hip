@@ -200,6 +200,10 @@ __global__ void __launch_bounds__(NB)
   const int64_t j0 = (int64_t)p * plen;
   const int64_t j1 = std::min<int64_t>(nx, j0 + plen);
   cdouble *xc = (cdouble *)X;
+  const double e2 = eps * eps;
+  // eps <= 0: sqrt(r) >= 0 is never below it (and eps^2 would be > 0)
+  const double e2lo = eps > 0 ? e2 * (1.0 - 0x1.0p-48) : -1.0;
+  const double e2hi = eps > 0 ? e2 * (1.0 + 0x1.0p-48) : -1.0;
   unsigned long long mine = 0;
   for (int64_t j = j0; j < j1; ++j) {
     double r;
@@ -207,9 +211,13 @@ __global__ void __launch_bounds__(NB)
       r = exact_sqdist_reg<MAXD>(qv, xc + j * ldx, d);
     else
       r = pw_sum(SqDiff<double>{qrow, X + j * ldx}, d);
-    // _vec_matrix_euclid computes row - sample; (a - b)^2 == (b - a)^2
-    const double dist = sqrt(r);
-    if (live && dist < eps) {
+    // _vec_matrix_euclid computes row - sample; (a - b)^2 == (b - a)^2.
+    // sqrt(r) < eps is decided on r where r is clear of eps^2 by a relative
+    // 2^-48 (far beyond the rounding of eps^2 and of the correctly rounded
+    // sqrt); the band between takes the reference's sqrt and compare.
+    const bool in = r < e2lo || (r <= e2hi && sqrt(r) < eps);
+    if (live && in) {
+      const double dist = sqrt(r);
       if constexpr (PASS == 0) {
         ++mine;
       } else {
@@ -217,6 +225,7 @@ __global__ void __launch_bounds__(NB)
         out_i[at] = j;
         out_d[at] = dist;
       }
+      (void)dist;
     }
   }
   if constexpr (PASS == 0)

@@ -135,6 +135,9 @@ def test_epsilon_query_reference_golden(name):
     (500, 100, 14.0, 30, 480, False),   # d > 64: query read from memory
     (1500, 2, 1.5, 0, 1500, True),      # integer grid: many equal distances
     (6000, 2, 1e9, 0, 3, False),        # lists of 6000 (> LDS sort cap)
+    (800, 2, 2.0, 0, 800, True),        # distances exactly eps (excluded)
+    (300, 3, 0.0, 0, 300, True),        # eps = 0: no neighbours at all
+    (300, 3, -1.0, 0, 300, False),      # negative eps: none either
 ])
 def test_epsilon_query_vs_oracle(n, d, eps, b, e, grid):
     rng = np.random.default_rng(n + d)
