@@ -147,7 +147,7 @@ def _cpu_task(block, centers):
 # one configuration on the GPU(s)
 # ---------------------------------------------------------------------------
 def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
-               mode, labels, n_blobs=None):
+               mode, labels, n_blobs=None, f32=False):
     from dislib_amd import _device, _shard
     from dislib_amd.cluster.kmeans import _Lloyd, _init_centers
     from dislib_amd.data import Dataset, Subset
@@ -155,6 +155,9 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
     X = torch.empty((n, d), dtype=torch.float64, device=dev)
     # global rows [rank*n, (rank+1)*n): the ranks shard one dataset
     _device.make_blobs(X, rank * n, n_blobs, seed=0, box=10.0, std=1.0)
+    if f32:                  # fp32 samples: fp64 distances, fp32 sums
+        X = X.to(torch.float32)
+        torch.cuda.empty_cache()
     ds = Dataset(n_features=d)
     for i in range(0, n, subset):
         ds.append(Subset(X[i:i + subset]))
@@ -192,7 +195,7 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
     return out
 
 
-def roofline(n, d, k, r, labels):
+def roofline(n, d, k, r, labels, es=8):
     """Roofline of the assignment call (the dominant kernels).  Small d:
     HBM-bound, algorithmic bytes = X read (8 d) + labels (delta path:
     previous label read 4 B + label write 4 B).  d > 128: MFMA-bound, the
@@ -222,7 +225,7 @@ def roofline(n, d, k, r, labels):
                "kernel_ms": r["kern_ms"],
                "alg_fp64_equiv_tflops": 2.0 * k * d * n / sec / 1e12,
                "fp64_peak_tflops": FP64_PEAK_TFLOPS,
-               "hbm_gbs": n * 8 * d / sec / 1e9}
+               "hbm_gbs": n * es * d / sec / 1e9}
     out["traffic"] = None
     return out
 
@@ -233,12 +236,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     extras = [] if a.only_headline else [
-        # (name, n, d, k, subset, steps, warmup)
+        # (name, n, d, k, subset, steps, warmup, fp32 samples)
         ("KMeans k=1000 on 125M x 64 fp64 dense per GPU (BASELINE "
          "configs[2] per-GPU shard; north-star target)",
-         125_000_000, 64, 1000, 1_000_000, 10, 2),
+         125_000_000, 64, 1000, 1_000_000, 10, 2, False),
         ("KMeans k=4096 on 10M x 1024 fp64 dense per GPU (BASELINE "
-         "configs[3], MFMA-bound)", 10_000_000, 1024, 4096, 1_000_000, 5, 3),
+         "configs[3], MFMA-bound)", 10_000_000, 1024, 4096, 1_000_000, 5, 3,
+         False),
+        ("KMeans k=4096 on 10M x 1024 fp32 dense per GPU (BASELINE "
+         "configs[3], fp32 variant reported separately)", 10_000_000, 1024,
+         4096, 1_000_000, 5, 3, True),
     ]
 
     # CPU baselines first, before anything touches the GPU: their worker
@@ -250,7 +257,9 @@ def main():
         share = cpu_share()       # before the workers' BLAS settings below
         cpu["head"] = cpu_baseline(a.d, a.k, a.cpu_seconds,
                                    _ic(a.d, False, a.k, 0), a.k, share)
-        for i, (_, n, d, k, *_r) in enumerate(extras):
+        for i, (_, n, d, k, *_r, f32) in enumerate(extras):
+            if f32:
+                continue          # the fp64 line's baseline covers the shape
             cpu[i] = cpu_baseline(d, k, a.cpu_seconds / 2,
                                   _ic(d, False, k, 0), k, share)
 
@@ -268,14 +277,15 @@ def main():
         fp = run_config(torch, dist, dev, rank, world, a.n, a.d, a.k,
                         a.subset, a.steps, a.warmup, a.mode, True)
     ex = []
-    for i, (name, n, d, k, sub, steps, warm) in enumerate(extras):
+    for i, (name, n, d, k, sub, steps, warm, f32) in enumerate(extras):
         rr = run_config(torch, dist, dev, rank, world, n, d, k, sub, steps,
-                        warm, a.mode, False)
+                        warm, a.mode, False, f32=f32)
         e = {"workload": name, "n_per_gpu": n, "d": d, "k": k,
+             "dtype": "f32 samples (f64 distances)" if f32 else "f64",
              "value": n * world * steps / rr["el"],
              "unit": "samples·iters/s", "ms_per_step": rr["el"] / steps * 1e3,
              "steps": steps, "warmup": warm,
-             "roofline": roofline(n, d, k, rr, False),
+             "roofline": roofline(n, d, k, rr, False, 4 if f32 else 8),
              "rechecked_samples": rr["rechecked"]}
         if i in cpu:
             cpu[i]["gpu_over_cpu"] = e["value"] / cpu[i]["value"]

@@ -202,6 +202,29 @@ def test_gemm_c4_shape_vs_exact_kernel():
     _close(sums[j], x[lab == j].sum(axis=0), 1e-12)
 
 
+def test_gemm_c4_shape_fp32_samples():
+    """The fp32 variant of configs[3] (reported separately by bench.py):
+    fp32 samples at d = 1024, k = 4096 on 20k rows -- fp64 distances, so
+    labels bit-exact against the exact kernel and the oracle; fp32 partial
+    sums within 1e-4 relative of the oracle's."""
+    d, k, n = 1024, 4096, 20000
+    x, _ = make_blobs(n_samples=n, n_features=d, centers=k,
+                      center_box=(-10, 10), random_state=16)
+    x = x.astype(np.float32)
+    rng = np.random.default_rng(5)
+    C = x[rng.choice(n, k, replace=False)].astype(np.float64) + \
+        rng.standard_normal((k, d))
+    lab, sums, cnt, _ = _run(x, C)
+    ref, _, _, _ = _run(x[:4000], C, mode="exact", kind="predict")
+    assert np.array_equal(lab[:4000], ref)
+    assert cnt.sum() == n
+    sub = rng.choice(n, 400, replace=False)
+    assert np.array_equal(lab[sub], orc.predict_labels(x[sub], C))
+    for j in np.argsort(cnt)[-3:]:
+        ref_sum = x[lab == j].sum(axis=0, dtype=np.float32)
+        _close(sums[j], ref_sum, 1e-4)
+
+
 def test_f15_c4mini_fit_predict_vs_reference():
     """Golden vectors of the reference's own KMeans at the C4 shape:
     make_blobs(20000 x 1024, 4096 centres), KMeans(4096, max_iter=2, tol=0,
