@@ -1330,9 +1330,11 @@ __global__ void __launch_bounds__(SBW) __attribute__((
 // per term -- xh.ch on v_mfma_f32_32x32x16_bf16 -- a third of bf16x3's
 // matrix work, with its own bound:
 //   x -> fl32 -> bf16 and -2c -> fl32 -> bf16 (round to nearest) lose
-//   <= 2^-9 each: 1.02 * 2^-8 sum|x (-2c)|; the fp32 chain of dpad products
-//   + |c|^2 (dpad + 2) 2^-23; packing 2^PACK1 ulp; numpy's rounding; all as
-//   screen_bound's terms, B doubled for safety.
+//   <= 2^-8 each (unit roundoff of an 8-bit significand), a product
+//   <= (2^-7 + 2^-16) |x (-2c)|; B = 2 (1.02 2^-8 + (16 NKS + 2) 2^-23) mag
+//   covers that, the fp32 chain of dpad products + |c|^2, packing 2^PACK1
+//   ulp and numpy's rounding (screen_bound's terms).  Unlike bf16x3's, this
+//   B is not doubled beyond the rigorous value: the slack is the 1.02.
 // The looser bound leaves ~5% of converged C3 samples undecided, nearly all
 // with exactly two candidates, so each lane keeps a packed top-3 (4 VALU
 // ops per score: pack, 2 x med3, min) and the decision is three-way:
@@ -1350,13 +1352,21 @@ __global__ void __launch_bounds__(SBW) __attribute__((
 // register prefetch of the next tile -- the CU's other waves cover a
 // wave's load (at 2 waves per SIMD with a prefetched tile the kernel waited
 // 48% of its cycles: PMC r02a)
-constexpr int SBB = 1024;
+#ifndef DKM_AB_SBB
+#define DKM_AB_SBB 768
+#endif
+constexpr int SBB = DKM_AB_SBB;
 constexpr uint32_t PACK1 = 9, PACK1_MASK = (1u << PACK1) - 1;
+// threshold pass: at most this many of a wave's 32 samples may end with an
+// over-full (or unusable) candidate list before the wave redoes the tile
+// with the top-3 pass
+constexpr int B1_RTHR = 4;
+
 template <class TX, int NKS>
 __global__ void __launch_bounds__(SBB)
     k_screen_b1(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
                 int k, WsView v, int32_t *__restrict__ lab_out, int64_t base,
-                int delta) {
+                int delta, int hint) {
   constexpr int GB = 1 << (PACK1 - 4);  // 32-centre blocks per group
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int nkb = (int)(kpad32(k) / 32);
@@ -1387,6 +1397,8 @@ __global__ void __launch_bounds__(SBB)
   int2 *cl = v.clist + wv * B1_CAP;  // 2 candidates
   const bool listing = wv < TL_SEGS && wv < B1_SEGS;
   int tl_cnt = 0, cl_cnt = 0, tl_over = 0;
+  uint32_t t_tiles = 0, t_done = 0;  // threshold passes run / accepted
+
 
   double tile[NKS][8];
   int pv = -1;
@@ -1398,41 +1410,48 @@ __global__ void __launch_bounds__(SBB)
         (void *)(X + std::min(s0, n) * ldx), 0,
         (int)std::min<int64_t>(rows * ldx * (int64_t)sizeof(TX), 0x7fffffff),
         0x00020000);
-    if (delta) {
+    if (delta || hint) {
       const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
           (void *)(lab_out + std::min(s0, n)), 0,
           (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
       pv = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
     }
+    // every load of the tile is issued unconditionally, so one wait covers
+    // them all (loads under a lane-dependent `16 ks + 8 h < d` branch each
+    // waited inside their branch: NKS serial HBM round trips per tile).
+    // Loads past the last row read 0 (num_records); features past d of a
+    // row read its successor and are zeroed below.
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      if (16 * ks + 8 * h < d) {
-        const int o = 16 * ks * (int)sizeof(TX);
-        if constexpr (sizeof(TX) == 8) {
+      const int o = 16 * ks * (int)sizeof(TX);
+      if constexpr (sizeof(TX) == 8) {
 #pragma unroll
-          for (int p4 = 0; p4 < 4; ++p4) {
-            const double2 v2 = __builtin_bit_cast(
-                double2, __builtin_amdgcn_raw_buffer_load_b128(
-                             rx, lane_off, o + 16 * p4, 0));
-            tile[ks][2 * p4] = v2.x;
-            tile[ks][2 * p4 + 1] = v2.y;
-          }
-        } else {
-#pragma unroll
-          for (int p4 = 0; p4 < 2; ++p4) {
-            const float4 v4 = __builtin_bit_cast(
-                float4, __builtin_amdgcn_raw_buffer_load_b128(
-                            rx, lane_off, o + 16 * p4, 0));
-            tile[ks][4 * p4] = v4.x;
-            tile[ks][4 * p4 + 1] = v4.y;
-            tile[ks][4 * p4 + 2] = v4.z;
-            tile[ks][4 * p4 + 3] = v4.w;
-          }
+        for (int p4 = 0; p4 < 4; ++p4) {
+          const double2 v2 = __builtin_bit_cast(
+              double2, __builtin_amdgcn_raw_buffer_load_b128(
+                           rx, lane_off, o + 16 * p4, 0));
+          tile[ks][2 * p4] = v2.x;
+          tile[ks][2 * p4 + 1] = v2.y;
         }
       } else {
 #pragma unroll
-        for (int m = 0; m < 8; ++m) tile[ks][m] = 0.0;
+        for (int p4 = 0; p4 < 2; ++p4) {
+          const float4 v4 = __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(
+                          rx, lane_off, o + 16 * p4, 0));
+          tile[ks][4 * p4] = v4.x;
+          tile[ks][4 * p4 + 1] = v4.y;
+          tile[ks][4 * p4 + 2] = v4.z;
+          tile[ks][4 * p4 + 3] = v4.w;
+        }
       }
+    }
+    if (d != 16 * NKS) {  // wave-uniform
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          tile[ks][m] = 16 * ks + 8 * h + m < d ? tile[ks][m] : 0.0;
     }
   };
 
@@ -1459,10 +1478,13 @@ __global__ void __launch_bounds__(SBB)
       xx = xa + xb;
     }
     const int prv = pv;
-
-    // running (value, centre) top-3 of this lane over all groups
-    float r1 = INFINITY, r2 = INFINITY, r3 = INFINITY;
-    int i1 = 0, i2 = 0, i3 = 0;
+    const int64_t si = s0 + r;
+    float xn;
+    const float B2 = bound2_fast(bk, xx, xn);
+    const bool sane0 = (xn < 1e18f) & (xn * cm < 1e30f);
+    bool unique = false, two = false;
+    int i1 = 0, i2 = 0;
+    bool need3 = true;
     auto chain = [&](int cb, f32x16 &accv) {
       const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
       const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
@@ -1477,90 +1499,234 @@ __global__ void __launch_bounds__(SBB)
                                                        0);
       }
     };
-    for (int g0 = 0; g0 < nkb; g0 += GB) {
-      const int g1 = min(nkb, g0 + GB);
-      // two independent packed top-3 chains (even / odd registers): half
-      // the dependency depth of one chain; merged at the group fold
-      float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
-      float e1 = INFINITY, e2 = INFINITY, e3 = INFINITY;
-      auto score = [&](int cb, const f32x16 &accv) {
-        const uint32_t t0 = opaque_s32((uint32_t)((cb - g0) * 16));
+    if (hint) {
+      // ---- threshold pass (label hint p = the sample's incoming label) ----
+      // s_hat_p: this sample's score against centre p from the same bf16
+      // operands (exact bf16 products, fp32 sums: within the single-product
+      // bound B = B2 / 2 of the reference distance, like every MFMA score).
+      // T = s_hat_p + B2: a centre j with s_j > T has D_j > D_p, so it is
+      // neither the reference winner nor tied with it.  Only the scores
+      // <= T are kept (the hint's own centre always is), so a lane spends
+      // one compare per score instead of the top-3's four ops.
+      const bool pok = prv >= 0 && prv < k;
+      const uint64_t bad = __ballot(!pok && s0 + r < n);
+      if (__popcll(bad) <= 2 * B1_RTHR) {
+        const int p = pok ? prv : 0;
+        const int pcb = p >> 5, pw = p & 31;
+        float dot = 0.f;
 #pragma unroll
-        for (int g = 0; g < 16; g += 2) {
-          const float sp =
-              __uint_as_float((__float_as_uint(accv[g]) & vmask) | (t0 + g));
-          const float sq = __uint_as_float(
-              (__float_as_uint(accv[g + 1]) & vmask) | (t0 + g + 1));
-          b3 = __builtin_amdgcn_fmed3f(b2, b3, sp);
-          b2 = __builtin_amdgcn_fmed3f(b1, b2, sp);
-          b1 = min_nc(b1, sp, ninf);
-          e3 = __builtin_amdgcn_fmed3f(e2, e3, sq);
-          e2 = __builtin_amdgcn_fmed3f(e1, e2, sq);
-          e1 = min_nc(e1, sq, ninf);
+        for (int ks = 0; ks < NKS; ++ks) {
+          const bf16x8 cp = *(const bf16x8 *)(frag + ((int64_t)pcb * NKS + ks) *
+                                                         1024 + (pw + 32 * h) * 16);
+#pragma unroll
+          for (int m = 0; m < 8; ++m)
+            dot = fmaf((float)xh[ks][m], (float)cp[m], dot);
         }
-      };
-      f32x16 acc_a, acc_b;
-      chain(g0, acc_a);
-      int cb = g0;
-      for (; cb + 2 <= g1; cb += 2) {  // ping-pong: no runtime-indexed arrays
-        chain(cb + 1, acc_b);
-        score(cb, acc_a);
-        if (cb + 2 < g1) chain(cb + 2, acc_a);
-        score(cb + 1, acc_b);
+        {
+          float da, db;
+          pair_xor<32>(dot, da, db);
+          dot = da + db;
+        }
+        const float sp =
+            cn[pcb * 32 + 16 * ((pw >> 2) & 1) + (pw & 3) + 4 * (pw >> 3)] + dot;
+        const float T = pok ? sp + B2 : -INFINITY;
+        // up to 3 kept (score, centre) per lane, in scan order; cnt counts all
+        float q0 = INFINITY, q1 = INFINITY, q2 = INFINITY;
+        int j0 = 0, j1 = 0, j2 = 0, cnt = 0;
+        // scores tested 4 registers at a time (min3 + min + one compare and
+        // branch), each register only inside a taken group
+        auto keep = [&](int cb, const f32x16 &accv) {
+#pragma unroll
+          for (int g4 = 0; g4 < 16; g4 += 4) {
+            const float mn = fminf(
+                __builtin_amdgcn_fmed3f(accv[g4], accv[g4 + 1], ninf) ,
+                __builtin_amdgcn_fmed3f(accv[g4 + 2], accv[g4 + 3], ninf));
+            if (mn <= T) {
+#pragma unroll
+              for (int g = g4; g < g4 + 4; ++g) {
+                const float sc = accv[g];
+                if (sc <= T) {
+                  const int ci = cb * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+                  q2 = cnt == 2 ? sc : q2;
+                  j2 = cnt == 2 ? ci : j2;
+                  q1 = cnt == 1 ? sc : q1;
+                  j1 = cnt == 1 ? ci : j1;
+                  q0 = cnt == 0 ? sc : q0;
+                  j0 = cnt == 0 ? ci : j0;
+                  ++cnt;
+                }
+              }
+            }
+          }
+        };
+        // two-stage pipeline over the centre blocks: the LDS reads of block
+        // cb + 1 (norms into its accumulator, fragments into registers) are
+        // issued before block cb is scored, and its MFMA chain after, so
+        // no MFMA waits on an LDS read issued just before it
+        auto rd = [&](int cb, bf16x8 (&f)[NKS], f32x16 &accv) {
+          const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
+          const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
+          accv = f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                        c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks)
+            f[ks] = *(const bf16x8 *)(frag + ((int64_t)cb * NKS + ks) * 1024 +
+                                      lane * 16);
+        };
+        auto mm = [&](const bf16x8 (&f)[NKS], f32x16 &accv) {
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks)
+            accv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[ks], xh[ks], accv,
+                                                           0, 0, 0);
+        };
+        {
+          f32x16 acc_a, acc_b;
+          bf16x8 fa[NKS], fb[NKS];
+          rd(0, fa, acc_a);
+          mm(fa, acc_a);
+          for (int cb = 0; cb < nkb; cb += 2) {  // wave-uniform conditions
+            const bool has1 = cb + 1 < nkb, has2 = cb + 2 < nkb;
+            if (has1) rd(cb + 1, fb, acc_b);
+            keep(cb, acc_a);
+            if (has1) mm(fb, acc_b);
+            if (has2) rd(cb + 2, fa, acc_a);
+            if (has1) keep(cb + 1, acc_b);
+            if (has2) mm(fa, acc_a);
+          }
+        }
+        // the sample's two lanes: union of their kept lists
+        int ocnt, oj0, oj1, oj2;
+        float oq0, oq1, oq2;
+        ocnt = __shfl_xor(cnt, 32, 64);
+        oq0 = __shfl_xor(q0, 32, 64);
+        oq1 = __shfl_xor(q1, 32, 64);
+        oq2 = __shfl_xor(q2, 32, 64);
+        oj0 = __shfl_xor(j0, 32, 64);
+        oj1 = __shfl_xor(j1, 32, 64);
+        oj2 = __shfl_xor(j2, 32, 64);
+        const bool over = cnt > 3 || ocnt > 3 || cnt + ocnt == 0 || !pok ||
+                          !sane0 || !(T < 1e30f);
+        // best by (score, centre) over the <= 6 kept, then how many lie
+        // within B2 of it (the reference winner is among those)
+        float sv[6] = {q0, q1, q2, oq0, oq1, oq2};
+        int cv[6] = {j0, j1, j2, oj0, oj1, oj2};
+        bool ok[6] = {cnt > 0, cnt > 1, cnt > 2, ocnt > 0, ocnt > 1, ocnt > 2};
+        float bs = INFINITY;
+        int bc = 0x7fffffff;
+#pragma unroll
+        for (int e = 0; e < 6; ++e)
+          if (ok[e] && (sv[e] < bs || (sv[e] == bs && cv[e] < bc))) {
+            bs = sv[e];
+            bc = cv[e];
+          }
+        int namb = 0, other = 0;
+#pragma unroll
+        for (int e = 0; e < 6; ++e)
+          if (ok[e] && !(sv[e] - bs > B2)) {
+            ++namb;
+            other = cv[e] != bc ? cv[e] : other;
+          }
+        const uint64_t mo = __ballot(over && s0 + r < n && h == 0);
+        ++t_tiles;
+        if (__popcll(mo) <= B1_RTHR) {
+          ++t_done;
+          need3 = false;
+          unique = !over && namb == 1;
+          two = !over && namb == 2;
+          i1 = bc;
+          i2 = other;
+        }
+
       }
-      if (cb < g1) score(cb, acc_a);
-      // fold the group's packed top-3 into the running (value, index) top-3
-      auto gidx = [&](float p) {
-        const uint32_t tg = __float_as_uint(p) & PACK1_MASK;
-        const int g = (int)(tg & 15);
-        return (g0 + (int)(tg >> 4)) * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
-      };
-      auto ins = [&](float p) {
-        const int pi = gidx(p);
-        const bool c1 = p < r1, c2 = p < r2, c3 = p < r3;
-        r3 = c2 ? r2 : (c3 ? p : r3);
-        i3 = c2 ? i2 : (c3 ? pi : i3);
-        r2 = c1 ? r1 : (c2 ? p : r2);
-        i2 = c1 ? i1 : (c2 ? pi : i2);
-        r1 = c1 ? p : r1;
-        i1 = c1 ? pi : i1;
-      };
-      ins(b1);
-      ins(b2);
-      ins(b3);
-      ins(e1);
-      ins(e2);
-      ins(e3);
     }
-    {  // merge the two lanes of a sample: the top-3 of both triples under
-       // the (value, index) order, so both lanes build the same triple
-      const float o1 = __shfl_xor(r1, 32, 64), o2 = __shfl_xor(r2, 32, 64),
-                  o3 = __shfl_xor(r3, 32, 64);
-      const int j1 = __shfl_xor(i1, 32, 64), j2 = __shfl_xor(i2, 32, 64),
-                j3 = __shfl_xor(i3, 32, 64);
-      auto lt = [](float a, int ia, float b, int ib) {
-        return a < b || (a == b && ia < ib);
-      };
-      auto ins3 = [&](float p, int pi) {
-        const bool c1 = lt(p, pi, r1, i1), c2 = lt(p, pi, r2, i2),
-                   c3 = lt(p, pi, r3, i3);
-        r3 = c2 ? r2 : (c3 ? p : r3);
-        i3 = c2 ? i2 : (c3 ? pi : i3);
-        r2 = c1 ? r1 : (c2 ? p : r2);
-        i2 = c1 ? i1 : (c2 ? pi : i2);
-        r1 = c1 ? p : r1;
-        i1 = c1 ? pi : i1;
-      };
-      ins3(o1, j1);
-      ins3(o2, j2);
-      ins3(o3, j3);
+    if (need3) {
+      // running (value, centre) top-3 of this lane over all groups
+      float r1 = INFINITY, r2 = INFINITY, r3 = INFINITY;
+      int ii1 = 0, ii2 = 0, ii3 = 0;
+      for (int g0 = 0; g0 < nkb; g0 += GB) {
+        const int g1 = min(nkb, g0 + GB);
+        // two independent packed top-3 chains (even / odd registers): half
+        // the dependency depth of one chain; merged at the group fold
+        float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
+        float e1 = INFINITY, e2 = INFINITY, e3 = INFINITY;
+        auto score = [&](int cb, const f32x16 &accv) {
+          const uint32_t t0 = opaque_s32((uint32_t)((cb - g0) * 16));
+  #pragma unroll
+          for (int g = 0; g < 16; g += 2) {
+            const float sp =
+                __uint_as_float((__float_as_uint(accv[g]) & vmask) | (t0 + g));
+            const float sq = __uint_as_float(
+                (__float_as_uint(accv[g + 1]) & vmask) | (t0 + g + 1));
+            b3 = __builtin_amdgcn_fmed3f(b2, b3, sp);
+            b2 = __builtin_amdgcn_fmed3f(b1, b2, sp);
+            b1 = min_nc(b1, sp, ninf);
+            e3 = __builtin_amdgcn_fmed3f(e2, e3, sq);
+            e2 = __builtin_amdgcn_fmed3f(e1, e2, sq);
+            e1 = min_nc(e1, sq, ninf);
+          }
+        };
+        f32x16 acc_a, acc_b;
+        chain(g0, acc_a);
+        int cb = g0;
+        for (; cb + 2 <= g1; cb += 2) {  // ping-pong: no runtime-indexed arrays
+          chain(cb + 1, acc_b);
+          score(cb, acc_a);
+          if (cb + 2 < g1) chain(cb + 2, acc_a);
+          score(cb + 1, acc_b);
+        }
+        if (cb < g1) score(cb, acc_a);
+        // fold the group's packed top-3 into the running (value, index) top-3
+        auto gidx = [&](float p) {
+          const uint32_t tg = __float_as_uint(p) & PACK1_MASK;
+          const int g = (int)(tg & 15);
+          return (g0 + (int)(tg >> 4)) * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+        };
+        auto ins = [&](float p) {
+          const int pi = gidx(p);
+          const bool c1 = p < r1, c2 = p < r2, c3 = p < r3;
+          r3 = c2 ? r2 : (c3 ? p : r3);
+          ii3 = c2 ? ii2 : (c3 ? pi : ii3);
+          r2 = c1 ? r1 : (c2 ? p : r2);
+          ii2 = c1 ? ii1 : (c2 ? pi : ii2);
+          r1 = c1 ? p : r1;
+          ii1 = c1 ? pi : ii1;
+        };
+        ins(b1);
+        ins(b2);
+        ins(b3);
+        ins(e1);
+        ins(e2);
+        ins(e3);
+      }
+      {  // merge the two lanes of a sample: the top-3 of both triples under
+         // the (value, index) order, so both lanes build the same triple
+        const float o1 = __shfl_xor(r1, 32, 64), o2 = __shfl_xor(r2, 32, 64),
+                    o3 = __shfl_xor(r3, 32, 64);
+        const int j1 = __shfl_xor(ii1, 32, 64), j2 = __shfl_xor(ii2, 32, 64),
+                  j3 = __shfl_xor(ii3, 32, 64);
+        auto lt = [](float a, int ia, float b, int ib) {
+          return a < b || (a == b && ia < ib);
+        };
+        auto ins3 = [&](float p, int pi) {
+          const bool c1 = lt(p, pi, r1, ii1), c2 = lt(p, pi, r2, ii2),
+                     c3 = lt(p, pi, r3, ii3);
+          r3 = c2 ? r2 : (c3 ? p : r3);
+          ii3 = c2 ? ii2 : (c3 ? pi : ii3);
+          r2 = c1 ? r1 : (c2 ? p : r2);
+          ii2 = c1 ? ii1 : (c2 ? pi : ii2);
+          r1 = c1 ? p : r1;
+          ii1 = c1 ? pi : ii1;
+        };
+        ins3(o1, j1);
+        ins3(o2, j2);
+        ins3(o3, j3);
+      }
+      const bool sane = sane0 & (r1 < 1e30f);
+      unique = sane & (r2 - r1 > B2);
+      two = sane & !unique & (r3 - r1 > B2);
+      i1 = ii1;
+      i2 = ii2;
     }
-    const int64_t si = s0 + r;
-    float xn;
-    const float B2 = bound2_fast(bk, xx, xn);
-    const bool sane = (xn < 1e18f) & (xn * cm < 1e30f) & (r1 < 1e30f);
-    const bool unique = sane & (r2 - r1 > B2);
-    const bool two = sane & !unique & (r3 - r1 > B2);
     const bool valid = si < n && h == 0;
     const int prev = delta ? prv : -1;
     // two candidates -> candidate list, more -> re-check list
@@ -1586,13 +1752,21 @@ __global__ void __launch_bounds__(SBB)
       tl_over += addt;
     }
     (void)spill;
-    if (valid && !(unique && i1 == prev))
+    // a label equal to the incoming one (the hint) needs no store
+    if (valid && !(unique && i1 == (hint ? prv : prev)))
       lab_out[si] = unique ? i1 : -(prev + 2);
   }
   if (lane == 0 && listing) {
     v.tcount[wv] = tl_cnt;
     v.ccount[wv] = cl_cnt;
   }
+  if (lane == 0 && t_tiles) {  // diagnostics (dkm_screen_counters)
+    atomicAdd((unsigned long long *)&v.hdr->reserved[0],
+              (unsigned long long)t_tiles);
+    atomicAdd((unsigned long long *)&v.hdr->reserved[1],
+              (unsigned long long)t_done);
+  }
+
   if (lane == 0 && tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
 }
 
@@ -2294,7 +2468,7 @@ static bool sums_fit_lds(int64_t k, int64_t d) {
 template <class TX>
 static int launch_screen_b1(const TX *X, int64_t end, int d, int64_t ldx,
                             int k, const WsView &v, int32_t *lab_out,
-                            int64_t base, hipStream_t s, int *nseg) {
+                            int64_t base, int hint, hipStream_t s, int *nseg) {
   const size_t lds = b1_frag_bytes(k, d);
   const int nks = (int)(dpad16(d) / 16);
   const void *kf = nullptr;
@@ -2322,7 +2496,7 @@ static int launch_screen_b1(const TX *X, int64_t end, int d, int64_t ldx,
 #define DKM_B1L(N)                                                          \
   case N:                                                                   \
     k_screen_b1<TX, N><<<g, SBB, lds, s>>>(X, end, d, ldx, k, v, lab_out,   \
-                                           base, delta);                    \
+                                           base, delta, hint);              \
     break;
     DKM_B1L(1) DKM_B1L(2) DKM_B1L(3) DKM_B1L(4)
     DKM_B1L(5) DKM_B1L(6) DKM_B1L(7) DKM_B1L(8)
@@ -2400,8 +2574,10 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
     int32_t *lab_out = labels ? labels : v.queue - base;
     int r, nseg = 0;
     if (b1) {
-      if ((r = launch_screen_b1<TX>(X, end, d, ldx, k, v, lab_out, base, s,
-                                    &nseg)))
+      // the incoming labels (previous iteration) seed the threshold pass
+      const int hint = labels && acc_kind != 0 ? 1 : 0;
+      if ((r = launch_screen_b1<TX>(X, end, d, ldx, k, v, lab_out, base, hint,
+                                    s, &nseg)))
         return r;
       r = launch_cand2<TX>(X, d, ldx, C, v, lab_out, base, nseg, s);
     } else if (w32)

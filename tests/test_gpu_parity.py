@@ -339,6 +339,67 @@ def test_partial_sum_vs_oracle(mode, n, d, k, seed):
     _close(sums, rs, 1e-12)
 
 
+def _partial_sum_hinted(x, C, hint, mode="bf16"):
+    """dkm_partial_sum with the label buffer pre-filled: the single-product
+    screen reads it as the threshold pass's hint (any content is legal)."""
+    from dislib_amd import _device, _lib
+    dev = torch.device("cuda", 0)
+    ds = _load(x, x.shape[0])
+    dd = ds._device_data()
+    k, d = C.shape
+    Ct = torch.from_numpy(np.ascontiguousarray(C)).to(dev)
+    ws = _device.Workspace(k, d, dd.n, dev)
+    acc = torch.empty(k * (d + 1), dtype=torch.float64, device=dev)
+    lab = torch.from_numpy(hint.astype(np.int32)).to(dev)
+    _device.prepare(Ct, ws, acc)
+    _device.partial_sum(dd, Ct, ws, lab, acc,
+                        {"bf16": _lib.MODE_BF16, "auto": _lib.MODE_AUTO}[mode])
+    a = acc.cpu().numpy()
+    return lab.cpu().numpy(), a[:k * d].reshape(k, d), a[k * d:], \
+        _device.rechecked(ws)
+
+
+@pytest.mark.parametrize("kind", ["exact", "noisy", "zeros", "invalid",
+                                  "stale", "dups", "tight"])
+def test_label_hint_threshold_pass(kind):
+    """The single-product screen's threshold pass (C3 shape: d = 64,
+    k = 1000) is exact whatever the incoming labels hold: the right labels,
+    30 % wrong, one centre for all, out-of-range values, labels of moved
+    centres, hints on the later of exactly duplicated centres (ties: the
+    first index must win), or a tight group of 100 centres (long candidate
+    lists: the top-3 fallback)."""
+    rng = np.random.default_rng(77)
+    n, d, k = 60000, 64, 1000
+    blobs = rng.uniform(-10, 10, (k, d))
+    x = blobs[rng.integers(0, k, n)] + rng.standard_normal((n, d))
+    C = blobs + rng.standard_normal((k, d)) * 0.3
+    if kind == "dups":
+        for a, b in [(3, 700), (10, 11), (500, 999)]:
+            C[b] = C[a]
+        C[12] = C[10] + 1e-7                 # near tie with 10 and 11
+    if kind == "tight":
+        # 100 centres packed around one point, 8 % of the samples near it:
+        # more than 3 candidates per lane (overflow: the top-3 fallback)
+        z = rng.uniform(-10, 10, d)
+        C[900:] = z + 0.05 * rng.standard_normal((100, d))
+        near = rng.random(n) < 0.08
+        x[near] = z + rng.standard_normal((int(near.sum()), d))
+    rl, rs, rc = orc.partial_sum(x, C)
+    hint = {"exact": rl,
+            "noisy": np.where(rng.random(n) < 0.3, rng.integers(0, k, n), rl),
+            "zeros": np.zeros(n, np.int64),
+            "invalid": rng.choice([-1, k, k + 5, -7, 3], n),
+            "stale": orc.predict_labels(x, C + rng.standard_normal((k, d))),
+            "dups": np.where(np.isin(rl, [3, 10, 500]),
+                             np.select([rl == 3, rl == 10, rl == 500],
+                                       [700, 11, 999]), rl),
+            "tight": rl}[kind]
+    lab, sums, cnt, _ = _partial_sum_hinted(x, C, np.asarray(hint))
+    assert np.array_equal(lab, rl)
+    assert np.array_equal(cnt, rc.astype(np.float64))
+    _close(sums, rs, 1e-12)
+
+
 @pytest.mark.parametrize("mode", ["screen32", "bf16x3", "bf16"])
 def test_screen_rechecks_only_ambiguous_samples(mode):
     rng = np.random.default_rng(21)
