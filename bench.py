@@ -195,6 +195,16 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
     return out
 
 
+def screen_products(k, d):
+    """bf16 MFMA products per term of the d <= 128 screen auto mode runs
+    (dkm_dense.hip `assign`: the single-product screen when k x d sums do
+    not fit an 80 KB LDS budget beside the fragments; bf16x3 otherwise)."""
+    lds_stride = d if d % 2 else d + 1
+    frags = ((k + 31) // 32) * (4096 + 128) if d <= 32 else \
+        ((k + 15) // 16) * (((d + 31) // 32) * 2048 + 64)
+    return 3 if frags + (k * lds_stride + k) * 8 <= 80 * 1024 else 1
+
+
 def roofline(n, d, k, r, labels, es=8):
     """Roofline of the assignment call (the dominant kernels).  Small d:
     HBM-bound, algorithmic bytes = X read (8 d) + labels (delta path:
@@ -211,8 +221,12 @@ def roofline(n, d, k, r, labels, es=8):
                "kernel": "dkm_assign_delta / dkm_partial_sum (screen + "
                          "re-check)",
                "kernel_ms": r["kern_ms"],
-               # bf16x3: 3 MFMA products per x.c term
-               "mfma_bf16_tflops_executed": 6.0 * k * d * n / sec / 1e12,
+               # MFMA products per x.c term of the screen auto mode picks:
+               # bf16x3 (3) when the fp64 sums fit LDS beside the centre
+               # fragments, else the single-product screen (1)
+               "mfma_products": screen_products(k, d),
+               "mfma_bf16_tflops_executed":
+                   2.0 * screen_products(k, d) * k * d * n / sec / 1e12,
                "mfma_bf16_peak_tflops": BF16_PEAK_TFLOPS}
     else:
         dp, kp = (d + 31) // 32 * 32, (k + 255) // 256 * 256
