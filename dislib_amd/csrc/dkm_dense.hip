@@ -1395,6 +1395,8 @@ __global__ void __launch_bounds__(SBB)
   const int64_t step = (int64_t)gridDim.x * (SBB / 64) * 32;
   int2 *wl = v.tlist + wv * TL_CAP;  // >= 3 candidates
   int2 *cl = v.clist + wv * B1_CAP;  // 2 candidates
+  int4 *nl = v.nlist + wv * B1_NCAP; // 3..6 candidates
+  int nl_cnt = 0;
   const bool listing = wv < TL_SEGS && wv < B1_SEGS;
   int tl_cnt = 0, cl_cnt = 0, tl_over = 0;
   uint32_t t_tiles = 0, t_done = 0;  // threshold passes run / accepted
@@ -1482,8 +1484,9 @@ __global__ void __launch_bounds__(SBB)
     float xn;
     const float B2 = bound2_fast(bk, xx, xn);
     const bool sane0 = (xn < 1e18f) & (xn * cm < 1e30f);
-    bool unique = false, two = false;
+    bool unique = false, two = false, many = false;
     int i1 = 0, i2 = 0;
+    uint32_t mpk0 = 0, mpk1 = 0, mpk2 = 0;  // many: the candidate set
     bool need3 = true;
     auto chain = [&](int cb, f32x16 &accv) {
       const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
@@ -1620,9 +1623,18 @@ __global__ void __launch_bounds__(SBB)
             bc = cv[e];
           }
         int namb = 0, other = 0;
+        uint32_t pk[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};
 #pragma unroll
         for (int e = 0; e < 6; ++e)
           if (ok[e] && !(sv[e] - bs > B2)) {
+            // the ambiguous members, packed 16 bits each in kept order
+#pragma unroll
+            for (int w = 0; w < 6; ++w)
+              if (w == namb)
+                pk[w >> 1] = (w & 1) ? (pk[w >> 1] & 0xffffu) |
+                                           ((uint32_t)cv[e] << 16)
+                                     : (pk[w >> 1] & 0xffff0000u) |
+                                           (uint32_t)cv[e];
             ++namb;
             other = cv[e] != bc ? cv[e] : other;
           }
@@ -1633,8 +1645,12 @@ __global__ void __launch_bounds__(SBB)
           need3 = false;
           unique = !over && namb == 1;
           two = !over && namb == 2;
+          many = !over && namb >= 3;
           i1 = bc;
           i2 = other;
+          mpk0 = pk[0];
+          mpk1 = pk[1];
+          mpk2 = pk[2];
         }
 
       }
@@ -1729,9 +1745,22 @@ __global__ void __launch_bounds__(SBB)
     }
     const bool valid = si < n && h == 0;
     const int prev = delta ? prv : -1;
+    // 3..6 candidates of the threshold pass -> the N-candidate list
+    bool nlisted = false;
+    {
+      const uint64_t mn = __ballot(valid && many);
+      const int addn = __popcll(mn);
+      if (addn && listing && nl_cnt + addn <= B1_NCAP) {
+        if (valid && many)
+          nl[nl_cnt + lane_prefix(mn)] =
+              make_int4((int)(si - base), (int)mpk0, (int)mpk1, (int)mpk2);
+        nl_cnt += addn;
+        nlisted = many;
+      }
+    }
     // two candidates -> candidate list, more -> re-check list
     const uint64_t mc = __ballot(valid && two);
-    const uint64_t mt = __ballot(valid && !unique && !two);
+    const uint64_t mt = __ballot(valid && !unique && !two && !nlisted);
     const int addc = __popcll(mc), addt = __popcll(mt);
     bool spill = false;  // list full: the label scan finds the sample
     if (listing && cl_cnt + addc <= B1_CAP) {
@@ -1744,21 +1773,23 @@ __global__ void __launch_bounds__(SBB)
       tl_over += addc;
     }
     if (listing && tl_cnt + addt <= TL_CAP) {
-      if (valid && !unique && !two)
+      if (valid && !unique && !two && !nlisted)
         wl[tl_cnt + lane_prefix(mt)] = make_int2((int)(si - base), prev);
       tl_cnt += addt;
     } else {
-      spill |= valid && !unique && !two;
+      spill |= valid && !unique && !two && !nlisted;
       tl_over += addt;
     }
     (void)spill;
-    // a label equal to the incoming one (the hint) needs no store
-    if (valid && !(unique && i1 == (hint ? prv : prev)))
+    // a label equal to the incoming one (the hint) needs no store; an
+    // N-listed sample keeps it until k_candn writes the winner
+    if (valid && !nlisted && !(unique && i1 == (hint ? prv : prev)))
       lab_out[si] = unique ? i1 : -(prev + 2);
   }
   if (lane == 0 && listing) {
     v.tcount[wv] = tl_cnt;
     v.ccount[wv] = cl_cnt;
+    v.ncount[wv] = nl_cnt;
   }
   if (lane == 0 && t_tiles) {  // diagnostics (dkm_screen_counters)
     atomicAdd((unsigned long long *)&v.hdr->reserved[0],
@@ -1819,6 +1850,61 @@ __global__ void __launch_bounds__(BLOCK)
       const double o = __shfl_xor(dist, 8, 64);  // the other candidate
       if (live && cs == 0 && j == 0)
         lab_out[si] = (o < dist || (o == dist && c2 < c1)) ? c2 : c1;
+    }
+  }
+  if (mine) atomicAdd((unsigned long long *)&v.hdr->rechecked_total, mine);
+}
+
+// 3..6-candidate samples of k_screen_b1's threshold pass: the reference
+// arithmetic on exactly those centres (every other centre is strictly
+// farther), best by (distance, index).  8 lanes per distance in numpy's
+// leaf order as k_cand2 (d % 8 == 0, d <= 128); 8 entries per wave pass.
+template <class TX>
+__global__ void __launch_bounds__(BLOCK)
+    k_candn(const TX *__restrict__ X, int d, int64_t ldx,
+            const double *__restrict__ C, WsView v,
+            int32_t *__restrict__ lab_out, int64_t base, int nseg) {
+  const int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+  const int64_t nwv = (int64_t)gridDim.x * (BLOCK / 64);
+  const int lane = threadIdx.x & 63;
+  const int e = lane >> 3, j = lane & 7;
+  const int nst = d >> 3;
+  unsigned long long mine = 0;
+  for (int64_t L = wv; L < (int64_t)nseg * (B1_NCAP / 64); L += nwv) {
+    const int64_t sg = L % nseg;
+    const int t0 = (int)(L / nseg) * 64;
+    const int cnt = v.ncount[sg];
+    if (t0 == 0 && lane == 0) mine += cnt;
+    if (t0 >= cnt) continue;  // wave-uniform
+    const int4 *list = v.nlist + sg * B1_NCAP + t0;
+    const int m = min(64, cnt - t0);
+    for (int q = 0; q < m; q += 8) {
+      const bool live = q + e < m;
+      const int4 it = list[live ? q + e : 0];
+      const int64_t si = base + it.x;
+      const TX *xr = X + si * ldx + j;
+      const uint32_t pk[3] = {(uint32_t)it.y, (uint32_t)it.z, (uint32_t)it.w};
+      double best = INFINITY;
+      int bi = -1;
+      for (int w = 0; w < 6; ++w) {
+        const int c = (int)((pk[w >> 1] >> (16 * (w & 1))) & 0xffffu);
+        if (c == 0xffff) break;
+        double r = 0.0;
+        const double *cr = C + (int64_t)c * d + j;
+        for (int i = 0; i < nst; ++i) {
+          const double df = (double)xr[8 * i] - cr[8 * i];
+          r = i ? r + df * df : df * df;
+        }
+        r = r + __shfl_xor(r, 1, 64);
+        r = r + __shfl_xor(r, 2, 64);
+        r = r + __shfl_xor(r, 4, 64);
+        const double dc = sqrt(r);
+        if (dc < best || (dc == best && c < bi) || bi < 0) {
+          best = dc;
+          bi = c;
+        }
+      }
+      if (live && j == 0) lab_out[si] = bi;
     }
   }
   if (mine) atomicAdd((unsigned long long *)&v.hdr->rechecked_total, mine);
@@ -2518,6 +2604,19 @@ static int launch_cand2(const TX *X, int d, int64_t ldx, const double *C,
   return check_launch("two-candidate re-check");
 }
 
+template <class TX>
+static int launch_candn(const TX *X, int d, int64_t ldx, const double *C,
+                        const WsView &v, int32_t *lab_out, int64_t base,
+                        int nseg, hipStream_t s) {
+  const int64_t units = (int64_t)nseg * (B1_NCAP / 64);
+  const int64_t g = std::max<int64_t>(
+      1, std::min<int64_t>((int64_t)dev_info().cus * 8,
+                           (units + BLOCK / 64 - 1) / (BLOCK / 64)));
+  k_candn<TX><<<(unsigned)g, BLOCK, 0, s>>>(X, d, ldx, C, v, lab_out, base,
+                                            nseg);
+  return check_launch("N-candidate re-check");
+}
+
 // Screen + exact re-check over [0, n).  Labels go to `labels` when given,
 // else to the workspace scratch (queue region), in chunks of its capacity.
 template <class TX>
@@ -2580,6 +2679,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                                     s, &nseg)))
         return r;
       r = launch_cand2<TX>(X, d, ldx, C, v, lab_out, base, nseg, s);
+      if (!r && hint) r = launch_candn<TX>(X, d, ldx, C, v, lab_out, base,
+                                           nseg, s);
     } else if (w32)
       r = launch_screen_w32<TX>(X, end, d, ldx, k, v, lab_out, acc, amode,
                                 base, lds, use_list, s, &nseg);

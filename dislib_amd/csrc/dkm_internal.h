@@ -72,6 +72,7 @@ __host__ __device__ inline int64_t ct_ld(int64_t k) { return (k + 15) / 16 * 16;
 // ---------------------------------------------------------------------------
 constexpr int B1_SEGS = 4096;          // >= 256 CUs x 8 waves
 constexpr int B1_CAP = 4096;           // candidate entries per screen wave
+constexpr int B1_NCAP = 1024;          // 3..6-candidate entries per wave
 constexpr size_t B1_LDS_MAX = 150 * 1024;
 
 __host__ __device__ inline int64_t dpad16(int64_t d);
@@ -112,6 +113,9 @@ struct WsView {
                     // K-steps per 32-centre block (k_screen_b1)
   int2 *clist;     // b1_ok: B1_SEGS x B1_CAP (offset, c1 | c2 << 16)
   int32_t *ccount; // b1_ok: entries used per screen wave
+  int4 *nlist;     // b1_ok: B1_SEGS x B1_NCAP (offset, 6 centres as 16-bit
+                   // pairs, 0xffff = none): 3..6-candidate samples
+  int32_t *ncount; // b1_ok: entries used per screen wave
   int2 *tlist;    // TL_SEGS x TL_CAP undecided (offset, prev) per screen wave
   int32_t *tcount; // TL_SEGS entries used per screen wave
   // GEMM screen (gemm_path only; else NULL)

@@ -67,6 +67,8 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
     b += round_up(kpad32(k) * dpad16(d) * 2, 256);  // b1frag
     b += (size_t)B1_SEGS * B1_CAP * 8;              // clist
     b += (size_t)B1_SEGS * 4;                       // ccount
+    b += (size_t)B1_SEGS * B1_NCAP * 16;            // nlist
+    b += (size_t)B1_SEGS * 4;                       // ncount
   }
   if (k <= SORT_KMAX) b += round_up((k + 1) * 4, 256) + 2 * round_up(k * 4, 256);
   b += 3 * round_up(n_queue * 4, 256);  // queue, sitems, smoved
@@ -112,6 +114,8 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   v->b1frag = nullptr;
   v->clist = nullptr;
   v->ccount = nullptr;
+  v->nlist = nullptr;
+  v->ncount = nullptr;
   if (gemm_path(k, d)) {
     const int64_t kp = kpad256(k), dp = dpad32(d), m = gemm_chunk(d);
     v->gchunk = m;
@@ -132,6 +136,10 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
     v->clist = (int2 *)p;
     p += (size_t)B1_SEGS * B1_CAP * 8;
     v->ccount = (int32_t *)p;
+    p += (size_t)B1_SEGS * 4;
+    v->nlist = (int4 *)p;
+    p += (size_t)B1_SEGS * B1_NCAP * 16;
+    v->ncount = (int32_t *)p;
     p += (size_t)B1_SEGS * 4;
   }
   v->soff = v->scur = v->scnt = nullptr;
