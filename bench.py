@@ -209,8 +209,8 @@ def roofline(n, d, k, r, labels, es=8):
     """Roofline of the assignment call (the dominant kernels).  Small d:
     HBM-bound, algorithmic bytes = X read (8 d) + labels (delta path:
     previous label read 4 B + label write 4 B).  d > 128: MFMA-bound, the
-    executed bf16x3 MFMA flops of the GEMM screen (3 products x 2 k d per
-    sample over the padded tiles) against the dense bf16 peak."""
+    executed MFMA flops of the single-product GEMM screen (2 k d per sample
+    over the padded tiles) against the dense bf16 peak."""
     sec = r["kern_ms"] * 1e-3
     if d <= 128:
         b = n * (8 * d + 8)
@@ -229,13 +229,16 @@ def roofline(n, d, k, r, labels, es=8):
                    2.0 * screen_products(k, d) * k * d * n / sec / 1e12,
                "mfma_bf16_peak_tflops": BF16_PEAK_TFLOPS}
     else:
-        dp, kp = (d + 31) // 32 * 32, (k + 255) // 256 * 256
-        f = 6.0 * kp * dp * n
+        # auto mode runs the single-product GEMM screen (bf16 hi x hi on
+        # hi-only tiles, features padded to 64)
+        dp, kp = (d + 63) // 64 * 64, (k + 255) // 256 * 256
+        f = 2.0 * kp * dp * n
         out = {"bound": "mfma", "achieved": f / sec / 1e12,
                "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                "frac": f / sec / 1e12 / BF16_PEAK_TFLOPS,
-               "kernel": "dkm_assign (bf16x3 GEMM screen + exact "
-                         "candidates + sums)",
+               "kernel": "dkm_assign (single-product bf16 GEMM screen + "
+                         "exact candidates + sums)",
+               "mfma_products": 1,
                "kernel_ms": r["kern_ms"],
                "alg_fp64_equiv_tflops": 2.0 * k * d * n / sec / 1e12,
                "fp64_peak_tflops": FP64_PEAK_TFLOPS,

@@ -2722,7 +2722,7 @@ template <class TX>
 static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
                        const double *C, int k, const WsView &v, size_t wsb,
                        int32_t *labels, double *acc, int acc_kind,
-                       hipStream_t s) {
+                       bool one, hipStream_t s) {
   (void)wsb;
   const int64_t nq = std::min<int64_t>(v.nq, INT32_MAX);
   if (!labels && nq < 1)
@@ -2742,7 +2742,7 @@ static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
     const int64_t end = std::min(n, base + chunk);
     int32_t *lab_out = labels ? labels : v.queue - base;
     int r = gemm_screen<TX>(X, base, end, d, ldx, C, k, v, lab_out,
-                            skind ? acc : nullptr, skind == 2, s);
+                            skind ? acc : nullptr, skind == 2, one, s);
     if (r) return r;
     if (post && (r = launch_post_sums<TX>(X, base, end, d, ldx, lab_out,
                                           prevbuf, k, acc, v, s)))
@@ -2767,21 +2767,22 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
   hipStream_t s = (hipStream_t)stream;
   if (mode == DKM_MODE_AUTO)
     mode = !screen_ok(k, d) && !gemm_path(k, d) ? DKM_MODE_EXACT
-           // sums beyond LDS and bf16 centres resident: the single product
-           : screen_ok(k, d) && b1_ok(k, d) && !sums_fit_lds(k, d)
+           // the GEMM screen (d > 128) and sums beyond LDS with the bf16
+           // centres resident: the single product
+           : gemm_path(k, d) ||
+                   (screen_ok(k, d) && b1_ok(k, d) && !sums_fit_lds(k, d))
                ? DKM_MODE_SCREEN_BF16
                : DKM_MODE_SCREEN_BF16X3;
   if (mode == DKM_MODE_EXACT)
     return launch_exact<TX>(X, n, (int)d, ldx, C, (int)k, labels, acc,
                             acc_kind, s);
-  if (mode == DKM_MODE_SCREEN_BF16X3 && gemm_path(k, d)) {
+  if ((mode == DKM_MODE_SCREEN_BF16X3 || mode == DKM_MODE_SCREEN_BF16) &&
+      gemm_path(k, d)) {
     WsView v;
     if (int r = ws_view(ws, wsb, k, d, &v)) return r;
     return launch_gemm<TX>(X, n, (int)d, ldx, C, (int)k, v, wsb, labels, acc,
-                           acc_kind, s);
+                           acc_kind, mode == DKM_MODE_SCREEN_BF16, s);
   }
-  if (mode == DKM_MODE_SCREEN_BF16 && gemm_path(k, d))
-    mode = DKM_MODE_SCREEN_BF16X3;  // the GEMM screen's own precision
   if (mode == DKM_MODE_SCREEN32 || mode == DKM_MODE_SCREEN_BF16X3 ||
       mode == DKM_MODE_SCREEN_BF16) {
     if (!screen_ok(k, d))

@@ -106,11 +106,13 @@ template <bool VEC, class TX>
 __global__ void __launch_bounds__(256)
     k_gemm_split(const TX *__restrict__ X, int64_t row0, int64_t nrows,
                  int64_t mrows, int d, int64_t ldx, int nks, double scale,
-                 char *__restrict__ out, float *__restrict__ xn) {
+                 char *__restrict__ out, float *__restrict__ xn, int one) {
   const int lane = threadIdx.x & 63, rr = lane >> 3, f = lane & 7;
   const int64_t wv = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nw = (int64_t)gridDim.x * 4;
-  const int ngrp = nks * 4;  // 8-feature groups
+  // 8-feature groups: 4 per 32-feature hi/lo stage, 8 per 64-feature
+  // hi-only stage (one)
+  const int ngrp = nks * (one ? 8 : 4);
   for (int64_t rb = wv * 8; rb < mrows; rb += nw * 8) {
     const int64_t row = rb + rr;
     const bool valid = row < nrows;
@@ -163,11 +165,19 @@ __global__ void __launch_bounds__(256)
         hw[q] = hu;
         lw[q] = __builtin_bit_cast(uint32_t, l2);
       }
-      const int ks = g >> 2, c = g & 3;
-      char *tile = out + (st * nks + ks) * (int64_t)GSTAGE + r * 128;
-      *(uint4 *)(tile + 16 * gslot(r, c)) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-      *(uint4 *)(tile + 16 * gslot(r, 4 + c)) =
-          make_uint4(lw[0], lw[1], lw[2], lw[3]);
+      if (one) {
+        const int ks = g >> 3, c = g & 7;
+        char *tile = out + (st * nks + ks) * (int64_t)GSTAGE + r * 128;
+        *(uint4 *)(tile + 16 * gslot(r, c)) =
+            make_uint4(hw[0], hw[1], hw[2], hw[3]);
+      } else {
+        const int ks = g >> 2, c = g & 3;
+        char *tile = out + (st * nks + ks) * (int64_t)GSTAGE + r * 128;
+        *(uint4 *)(tile + 16 * gslot(r, c)) =
+            make_uint4(hw[0], hw[1], hw[2], hw[3]);
+        *(uint4 *)(tile + 16 * gslot(r, 4 + c)) =
+            make_uint4(lw[0], lw[1], lw[2], lw[3]);
+      }
     }
     ss += __shfl_xor(ss, 1, 64);
     ss += __shfl_xor(ss, 2, 64);
@@ -191,6 +201,7 @@ __global__ void k_gemm_cnorm(const float *__restrict__ cn32, int64_t k,
 // 32x32x16 accumulator register g of lane (r, h): centre row
 // (g & 3) + 8 (g >> 2) + 4h of the block, sample column r.
 // ---------------------------------------------------------------------------
+template <int NP>  // MFMA products per term: 3 (bf16x3) or 1 (hi x hi)
 __global__ void __launch_bounds__(GTHREADS)
     k_gemm_screen(const char *__restrict__ afrag, const float *__restrict__ gcn,
                   const char *__restrict__ xs, int nst, int nct, int nks,
@@ -268,20 +279,22 @@ __global__ void __launch_bounds__(GTHREADS)
     const char *la = lds + buf * (2 * GSTAGE);
     const char *lb = la + GSTAGE;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int oh = s ? oh1 : oh0, ol = s ? ol1 : ol0;
+    for (int s = 0; s < (NP == 1 ? 4 : 2); ++s) {
+      // hi-only rows (NP == 1): K-substep s reads hi chunk 2s + h
+      const int oh = NP == 1 ? 16 * ((2 * s + h) ^ sw) : (s ? oh1 : oh0);
+      const int ol = s ? ol1 : ol0;
       bf16x8 ah[4], al[4], bh[2], bl[2];
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) {
         const char *p = la + arow + mb * 32 * 128;
         ah[mb] = *(const bf16x8 *)(p + oh);
-        al[mb] = *(const bf16x8 *)(p + ol);
+        if constexpr (NP == 3) al[mb] = *(const bf16x8 *)(p + ol);
       }
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         const char *p = lb + brow + nb * 32 * 128;
         bh[nb] = *(const bf16x8 *)(p + oh);
-        bl[nb] = *(const bf16x8 *)(p + ol);
+        if constexpr (NP == 3) bl[nb] = *(const bf16x8 *)(p + ol);
       }
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb)
@@ -289,18 +302,20 @@ __global__ void __launch_bounds__(GTHREADS)
         for (int nb = 0; nb < 2; ++nb)
           acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
               ah[mb], bh[nb], acc[mb][nb], 0, 0, 0);
+      if constexpr (NP == 3) {
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb)
+        for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              ah[mb], bl[nb], acc[mb][nb], 0, 0, 0);
+          for (int nb = 0; nb < 2; ++nb)
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                ah[mb], bl[nb], acc[mb][nb], 0, 0, 0);
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb)
+        for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              al[mb], bh[nb], acc[mb][nb], 0, 0, 0);
+          for (int nb = 0; nb < 2; ++nb)
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                al[mb], bh[nb], acc[mb][nb], 0, 0, 0);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // buffer `buf` is free for stage ks + 2
@@ -357,11 +372,18 @@ __global__ void __launch_bounds__(GTHREADS)
   }
 }
 
-// 2B of the decision test (B = twice the rigorous bound; header comment)
-__device__ __forceinline__ float gemm_bound2(int dpad, float xn, float cm) {
-  const float rel = 0x1.0p-16f +
-                    (3.0f * dpad + 2.0f) * 0x1.0p-23f * (1.0f + 0x1.0p-7f) +
-                    0x1.0p-17f;
+// 2B of the decision test (B = twice the rigorous bound; header comment).
+// one: the single-product screen (hi x hi): x and -2c rounded to bf16 lose
+// <= 2^-8 each, a product <= (2^-7 + 2^-16) |x (-2c)| (1.02 2^-7 used),
+// the fp32 chain has dpad products.
+__device__ __forceinline__ float gemm_bound2(int dpad, float xn, float cm,
+                                            bool one) {
+  const float rel =
+      one ? 1.02f * 0x1.0p-7f +
+                (dpad + 2.0f) * 0x1.0p-23f * (1.0f + 0x1.0p-7f) + 0x1.0p-17f
+          : 0x1.0p-16f +
+                (3.0f * dpad + 2.0f) * 0x1.0p-23f * (1.0f + 0x1.0p-7f) +
+                0x1.0p-17f;
   const float s = xn + cm;
   const float mag = 2.0f * xn * cm + cm * cm;
   const float b = rel * mag + 0x1.0p-48f * s * s +
@@ -378,7 +400,7 @@ struct GDecision {
 };
 __device__ __forceinline__ GDecision gemm_decide(const int2 *pp, int nct,
                                                  int dpad, float xn,
-                                                 float cm) {
+                                                 float cm, bool one) {
   float p1 = INFINITY;
   int i1 = 0x7fffffff;
   for (int e = 0; e < nct * GTOP; e += GTOP) {
@@ -391,7 +413,7 @@ __device__ __forceinline__ GDecision gemm_decide(const int2 *pp, int nct,
   }
   GDecision g;
   g.best = i1;
-  g.lim = p1 + gemm_bound2(dpad, xn, cm);
+  g.lim = p1 + gemm_bound2(dpad, xn, cm, one);
   g.ncand = 0;
   // NaN / overflow: no bound holds -> incomplete (exact path)
   g.complete = (xn < 1e18f) & (xn * cm < 1e30f) & (p1 < 1e30f);
@@ -536,7 +558,8 @@ __global__ void __launch_bounds__(256)
     int prev = -1;
     if (i < nrows) {
       const GDecision g =
-          gemm_decide(part + i * (int64_t)nct * GTOP, nct, dpad, xnv[i], cm);
+          gemm_decide(part + i * (int64_t)nct * GTOP, nct, dpad, xnv[i], cm,
+                      flags & 4);
       const int64_t si = row0 + i;
       prev = (flags & 2) ? lab_out[si] : -1;
       if (g.complete && g.ncand == 1) {
@@ -613,7 +636,7 @@ __global__ void __launch_bounds__(256)
         i1 = oi;
       }
     }
-    const float lim = p1 + gemm_bound2(dpad, xnv[i], cm);
+    const float lim = p1 + gemm_bound2(dpad, xnv[i], cm, flags & 4);
     const TX *xr = X + si * ldx;
     double best = INFINITY;
     int lab = 0x7fffffff;  // lanes without a candidate never win
@@ -714,17 +737,17 @@ __global__ void __launch_bounds__(1024)
 template <class TX>
 int launch_split(const TX *X, int64_t row0, int64_t nrows, int64_t mrows,
                  int d, int64_t ldx, double scale, char *out, float *xn,
-                 hipStream_t s) {
-  const int nks = (int)(dpad32(d) / GBK);
+                 int one, hipStream_t s) {
+  const int nks = one ? (int)(dpad64(d) / 64) : (int)(dpad32(d) / GBK);
   const bool vec = (d % 8 == 0) && ((ldx * (int64_t)sizeof(TX)) % 16 == 0) &&
                    ((uintptr_t)X % 16 == 0);
   const int64_t blocks = std::min<int64_t>((mrows + 31) / 32, 16384);
   if (vec)
     k_gemm_split<true, TX><<<(unsigned)blocks, 256, 0, s>>>(
-        X, row0, nrows, mrows, d, ldx, nks, scale, out, xn);
+        X, row0, nrows, mrows, d, ldx, nks, scale, out, xn, one);
   else
     k_gemm_split<false, TX><<<(unsigned)blocks, 256, 0, s>>>(
-        X, row0, nrows, mrows, d, ldx, nks, scale, out, xn);
+        X, row0, nrows, mrows, d, ldx, nks, scale, out, xn, one);
   return check_launch("gemm split");
 }
 
@@ -735,7 +758,10 @@ int gemm_prepare(const double *C, int64_t k, int64_t d, const WsView &v,
   if (!v.gfrag) return fail(DKM_E_WORKSPACE, "gemm_prepare: no GEMM region");
   const int64_t kp = kpad256(k);
   if (int r = launch_split<double>(C, 0, k, kp, (int)d, d, -2.0, v.gfrag,
-                                   nullptr, s))
+                                   nullptr, 0, s))
+    return r;
+  if (int r = launch_split<double>(C, 0, k, kp, (int)d, d, -2.0, v.gfrag1,
+                                   nullptr, 1, s))
     return r;
   k_gemm_cnorm<<<(unsigned)((kp + 255) / 256), 256, 0, s>>>(v.cn32, k, kp,
                                                             v.gcn);
@@ -745,25 +771,32 @@ int gemm_prepare(const double *C, int64_t k, int64_t d, const WsView &v,
 template <class TX>
 int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
                 const double *C, int k, const WsView &v, int32_t *lab_out,
-                double *acc, bool delta, hipStream_t s) {
+                double *acc, bool delta, bool one, hipStream_t s) {
   if (!v.gfrag) return fail(DKM_E_WORKSPACE, "gemm_screen: no GEMM region");
-  if (hipFuncSetAttribute((const void *)k_gemm_screen,
-                          hipFuncAttributeMaxDynamicSharedMemorySize,
+  const void *kf = one ? (const void *)k_gemm_screen<1>
+                       : (const void *)k_gemm_screen<3>;
+  if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
                           GLDS) != hipSuccess)
     return fail(DKM_E_LAUNCH, "gemm_screen: LDS attribute");
-  const int nks = (int)(dpad32(d) / GBK);
+  // single product: hi-only tiles, 64 features per stage
+  const int nks = one ? (int)(dpad64(d) / 64) : (int)(dpad32(d) / GBK);
   const int nct = (int)(kpad256(k) / GT);
-  const int dpad = (int)dpad32(d);
-  const int flags = (acc ? 1 : 0) | (delta ? 2 : 0);
+  const int dpad = one ? (int)dpad64(d) : (int)dpad32(d);
+  // bit 2: the single-product bound in the merge and candidate steps
+  const int flags = (acc ? 1 : 0) | (delta ? 2 : 0) | (one ? 4 : 0);
   for (int64_t c0 = base; c0 < end; c0 += v.gchunk) {
     const int64_t rows = std::min<int64_t>(v.gchunk, end - c0);
     const int64_t mrows = round_up(rows, GT);
     const int nst = (int)(mrows / GT);
     if (int r = launch_split<TX>(X, c0, rows, mrows, d, ldx, 1.0, v.gxs,
-                                 v.gxn, s))
+                                 v.gxn, one ? 1 : 0, s))
       return r;
-    k_gemm_screen<<<(unsigned)(nst * nct), GTHREADS, GLDS, s>>>(
-        v.gfrag, v.gcn, v.gxs, nst, nct, nks, v.gpart);
+    if (one)
+      k_gemm_screen<1><<<(unsigned)(nst * nct), GTHREADS, GLDS, s>>>(
+          v.gfrag1, v.gcn, v.gxs, nst, nct, nks, v.gpart);
+    else
+      k_gemm_screen<3><<<(unsigned)(nst * nct), GTHREADS, GLDS, s>>>(
+          v.gfrag, v.gcn, v.gxs, nst, nct, nks, v.gpart);
     if (int r = check_launch("gemm screen")) return r;
     // both list counters (gcount, gcount2: adjacent words)
     if (hipMemsetAsync(&v.hdr->gcount, 0, 8, s) != hipSuccess)
@@ -793,9 +826,10 @@ int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
 
 template int gemm_screen<double>(const double *, int64_t, int64_t, int,
                                  int64_t, const double *, int, const WsView &,
-                                 int32_t *, double *, bool, hipStream_t);
+                                 int32_t *, double *, bool, bool,
+                                 hipStream_t);
 template int gemm_screen<float>(const float *, int64_t, int64_t, int, int64_t,
                                 const double *, int, const WsView &,
-                                int32_t *, double *, bool, hipStream_t);
+                                int32_t *, double *, bool, bool, hipStream_t);
 
 }  // namespace dkm

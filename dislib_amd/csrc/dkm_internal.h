@@ -120,6 +120,8 @@ struct WsView {
   int32_t *tcount; // TL_SEGS entries used per screen wave
   // GEMM screen (gemm_path only; else NULL)
   char *gfrag;     // kpad256 x dpad32 centre tiles (-2c, bf16 hi/lo)
+  char *gfrag1;    // kpad256 x dpad64 centre tiles (-2c, bf16 hi only:
+                   // 64 features per 128-B row, the single-product screen)
   float *gcn;      // kpad256 fp32 ||c||^2, 2^100 for padding centres
   char *gxs;       // gemm_chunk samples: split tiles of the current chunk
   float *gxn;      // gemm_chunk fp32 upper bounds of ||x||
@@ -161,6 +163,7 @@ __host__ __device__ inline int64_t kpad16(int64_t k) { return (k + 15) / 16 * 16
 __host__ __device__ inline int64_t kpad32(int64_t k) { return (k + 31) / 32 * 32; }
 __host__ __device__ inline int64_t dpad16(int64_t d) { return (d + 15) / 16 * 16; }
 __host__ __device__ inline int64_t dpad32(int64_t d) { return (d + 31) / 32 * 32; }
+__host__ __device__ inline int64_t dpad64(int64_t d) { return (d + 63) / 64 * 64; }
 
 size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue);
 int64_t default_queue(int64_t k, int64_t d);
@@ -357,6 +360,6 @@ int gemm_prepare(const double *C, int64_t k, int64_t d, const WsView &v,
 template <class TX>
 int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
                 const double *C, int k, const WsView &v, int32_t *lab_out,
-                double *acc, bool delta, hipStream_t s);
+                double *acc, bool delta, bool one, hipStream_t s);
 
 }  // namespace dkm
