@@ -1,6 +1,7 @@
-"""GPU parity of the large-d path (d > 128): the bf16x3 MFMA GEMM screen
-(dkm_gemm.hip) + exact candidate evaluation + exact re-check, against the
-CPU oracle and against golden vectors produced by the reference itself.
+"""GPU parity of the large-d path (d > 128): the MFMA GEMM screen
+(dkm_gemm.hip; bf16x3, and the single-product mode auto picks) + exact
+candidate evaluation + exact re-check, against the CPU oracle and against
+golden vectors produced by the reference itself.
 
 Bar (BASELINE.json north star): labels bit-exact; centres within 1e-9
 relative in fp64 (1e-4 for fp32 samples); sums within 1e-12 of the oracle's
@@ -50,7 +51,7 @@ def _run(x, C, mode="bf16x3", kind="partial", prev=None):
     ws = _device.Workspace(k, d, dd.n, dev)
     acc = torch.zeros(k * (d + 1), dtype=torch.float64, device=dev)
     m = {"exact": _lib.MODE_EXACT, "bf16x3": _lib.MODE_BF16X3,
-         "auto": _lib.MODE_AUTO}[mode]
+         "bf16": _lib.MODE_BF16, "auto": _lib.MODE_AUTO}[mode]
     _device.prepare(Ct, ws, acc)
     if kind == "partial":
         lab = torch.full((dd.n,), -7, dtype=torch.int32, device=dev)
@@ -83,20 +84,22 @@ def _data(n, d, k, seed, dtype=np.float64):
     (600, 2048, 64, 5),      # 64 K-stages
     (70, 160, 9, 6),         # a single partial sample tile
 ])
-def test_gemm_partial_sum_vs_oracle(n, d, k, seed):
+@pytest.mark.parametrize("gmode", ["bf16x3", "bf16"])
+def test_gemm_partial_sum_vs_oracle(n, d, k, seed, gmode):
     x, C = _data(n, d, k, seed)
-    lab, sums, cnt, _ = _run(x, C)
+    lab, sums, cnt, _ = _run(x, C, mode=gmode)
     rl, rs, rc = orc.partial_sum(x, C)
     assert np.array_equal(lab, rl)
     assert np.array_equal(cnt, rc.astype(np.float64))
     _close(sums, rs, 1e-12)
-    plab, _, _, _ = _run(x, C, kind="predict")
+    plab, _, _, _ = _run(x, C, mode=gmode, kind="predict")
     assert np.array_equal(plab, rl)
 
 
-def test_gemm_fp32_samples():
+@pytest.mark.parametrize("gmode", ["bf16x3", "bf16"])
+def test_gemm_fp32_samples(gmode):
     x, C = _data(3000, 300, 100, 7, np.float32)
-    lab, sums, cnt, _ = _run(x, C)
+    lab, sums, cnt, _ = _run(x, C, mode=gmode)
     rl, rs, rc = orc.partial_sum(x, C)
     assert np.array_equal(lab, rl)
     assert np.array_equal(cnt, rc.astype(np.float64))
@@ -104,10 +107,11 @@ def test_gemm_fp32_samples():
 
 
 @pytest.mark.parametrize("d,k", [(200, 300), (1024, 600)])
-def test_gemm_delta_equals_difference_of_partial_sums(d, k):
+@pytest.mark.parametrize("gmode", ["bf16x3", "bf16"])
+def test_gemm_delta_equals_difference_of_partial_sums(d, k, gmode):
     x, C = _data(4000, d, k, d + k)
     prev = np.random.default_rng(1).integers(-1, k, x.shape[0])
-    lab, sums, cnt, _ = _run(x, C, kind="delta", prev=prev)
+    lab, sums, cnt, _ = _run(x, C, mode=gmode, kind="delta", prev=prev)
     rl, rs, rc = orc.partial_sum(x, C)
     assert np.array_equal(lab, rl)
     ps = np.zeros((k, d))
@@ -119,7 +123,8 @@ def test_gemm_delta_equals_difference_of_partial_sums(d, k):
     assert np.array_equal(cnt, rc - pc)
 
 
-def test_gemm_candidate_and_recheck_branches():
+@pytest.mark.parametrize("gmode", ["bf16x3", "bf16"])
+def test_gemm_candidate_and_recheck_branches(gmode):
     """Force every decision branch of the merge: (a) several centres within
     the bound in DIFFERENT centre tiles (complete candidate list: exact
     evaluation of the candidates), (b) more than 3 near-identical centres
@@ -143,7 +148,7 @@ def test_gemm_candidate_and_recheck_branches():
         xs.append(C[c] + 0.01 * rng.standard_normal((200, d)))
     xs.append(rng.uniform(-4, 4, (400, d)))
     x = np.vstack(xs)
-    lab, sums, cnt, nre = _run(x, C)
+    lab, sums, cnt, nre = _run(x, C, mode=gmode)
     rl, rs, rc = orc.partial_sum(x, C)
     assert np.array_equal(lab, rl)
     assert np.array_equal(cnt, rc.astype(np.float64))
@@ -152,7 +157,8 @@ def test_gemm_candidate_and_recheck_branches():
 
 
 @pytest.mark.parametrize("scale", [1e-30, 1e-3, 1.0, 1e6])
-def test_gemm_near_ties_across_scales(scale):
+@pytest.mark.parametrize("gmode", ["bf16x3", "bf16"])
+def test_gemm_near_ties_across_scales(scale, gmode):
     rng = np.random.default_rng(int(np.log10(scale) + 60))
     d, k = 192, 40
     C = rng.uniform(-10, 10, (k, d)) * scale
@@ -166,23 +172,25 @@ def test_gemm_near_ties_across_scales(scale):
             10.0 ** -rng.integers(6, 16)
         xs.append(0.5 * (C[a] + C[b]) + 0.2 * scale * w + eps * u)
     x = np.array(xs)
-    lab, _, _, _ = _run(x, C)
+    lab, _, _, _ = _run(x, C, mode=gmode)
     assert np.array_equal(lab, orc.predict_labels(x, C))
 
 
-def test_gemm_nonfinite_samples_go_exact():
+@pytest.mark.parametrize("gmode", ["bf16x3", "bf16"])
+def test_gemm_nonfinite_samples_go_exact(gmode):
     x, C = _data(1000, 160, 20, 12)
     x[3, 7] = np.nan
     x[9, 0] = np.inf
     x[11] = 1e200
-    lab, _, _, _ = _run(x, C)
+    lab, _, _, _ = _run(x, C, mode=gmode)
     ok = np.isfinite(x).all(axis=1)
     rl = orc.predict_labels(x, C)
     assert np.array_equal(lab, rl)
     assert ok.sum() == 998
 
 
-def test_gemm_c4_shape_vs_exact_kernel():
+@pytest.mark.parametrize("gmode", ["bf16x3", "bf16"])
+def test_gemm_c4_shape_vs_exact_kernel(gmode):
     """d = 1024, k = 4096 (BASELINE configs[3]) on 20k samples: every label
     against the exact kernel (the reference arithmetic for every pair, pinned
     to the oracle by the parity tests), 400 of them against the oracle."""
@@ -191,7 +199,7 @@ def test_gemm_c4_shape_vs_exact_kernel():
                       center_box=(-10, 10), random_state=15)
     rng = np.random.default_rng(4)
     C = x[rng.choice(n, k, replace=False)] + rng.standard_normal((k, d))
-    lab, sums, cnt, _ = _run(x, C)
+    lab, sums, cnt, _ = _run(x, C, mode=gmode)
     ref, _, _, _ = _run(x[:4000], C, mode="exact", kind="predict")
     assert np.array_equal(lab[:4000], ref)
     assert cnt.sum() == n
@@ -202,7 +210,8 @@ def test_gemm_c4_shape_vs_exact_kernel():
     _close(sums[j], x[lab == j].sum(axis=0), 1e-12)
 
 
-def test_gemm_c4_shape_fp32_samples():
+@pytest.mark.parametrize("gmode", ["bf16x3", "bf16"])
+def test_gemm_c4_shape_fp32_samples(gmode):
     """The fp32 variant of configs[3] (reported separately by bench.py):
     fp32 samples at d = 1024, k = 4096 on 20k rows -- fp64 distances, so
     labels bit-exact against the exact kernel and the oracle; fp32 partial
@@ -214,7 +223,7 @@ def test_gemm_c4_shape_fp32_samples():
     rng = np.random.default_rng(5)
     C = x[rng.choice(n, k, replace=False)].astype(np.float64) + \
         rng.standard_normal((k, d))
-    lab, sums, cnt, _ = _run(x, C)
+    lab, sums, cnt, _ = _run(x, C, mode=gmode)
     ref, _, _, _ = _run(x[:4000], C, mode="exact", kind="predict")
     assert np.array_equal(lab[:4000], ref)
     assert cnt.sum() == n
