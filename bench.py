@@ -58,7 +58,7 @@ def parse():
                    help="skip the CPU baselines")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--traffic-json", default=os.path.join(
-        ROOT, "profiles", "r01_traffic.json"))
+        ROOT, "profiles", "r02_traffic.json"))
     return p.parse_args()
 
 
