@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--n", type=int, default=100_000_000,
+    p.add_argument("--n", "--rows", dest="n", type=int, default=100_000_000,
                    help="samples per GPU (headline config)")
     p.add_argument("--d", type=int, default=32)
     p.add_argument("--k", type=int, default=100)
@@ -57,6 +57,12 @@ def parse():
     p.add_argument("--no-cpu", action="store_true",
                    help="skip the CPU baselines")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--extras-scale", type=float, default=1.0,
+                   help="scale the extra configs' rows per GPU (rehearsals "
+                        "only; their lines then name the scaled size)")
+    p.add_argument("--backend", default="nccl",
+                   help="process-group backend for N > 1 (nccl = RCCL; gloo "
+                        "only to rehearse several ranks on one GPU)")
     p.add_argument("--traffic-json", default=os.path.join(
         ROOT, "profiles", "r02_traffic.json"))
     return p.parse_args()
@@ -188,7 +194,7 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
     out = {"el": el, "kern_ms": kern_ms, "rechecked": st.rechecked(),
-           "collective": ("libdkm-rccl" if _shard._COMM else
+           "collective": ("libdkm-rccl" if any(_shard._COMM.values()) else
                           "torch.distributed") if world > 1 else "none"}
     del st, ds, X
     torch.cuda.empty_cache()
@@ -282,10 +288,15 @@ def main():
 
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU; a rehearsal with more ranks than GPUs (gloo) shares
+    ndev = max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.backend)
 
     r = run_config(torch, dist, dev, rank, world, a.n, a.d, a.k, a.subset,
                    a.steps, a.warmup, a.mode, a.labels)
@@ -295,6 +306,9 @@ def main():
                         a.subset, a.steps, a.warmup, a.mode, True)
     ex = []
     for i, (name, n, d, k, sub, steps, warm, f32) in enumerate(extras):
+        if a.extras_scale != 1.0:
+            n = max(sub, int(n * a.extras_scale) // sub * sub)
+            name += " [scaled to %d rows per GPU]" % n
         rr = run_config(torch, dist, dev, rank, world, n, d, k, sub, steps,
                         warm, a.mode, False, f32=f32)
         e = {"workload": name, "n_per_gpu": n, "d": d, "k": k,

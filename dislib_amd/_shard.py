@@ -62,7 +62,8 @@ def shard_dataset(dataset, rank=None, world_size=None):
     return out
 
 
-_COMM = {}   # device index -> True once libdkm's RCCL communicator is up
+_COMM = {}   # device index -> True once libdkm's RCCL communicator is up,
+             # False when the ranks agreed to use torch.distributed instead
 
 
 def _dkm_comm(t, d):
@@ -76,7 +77,7 @@ def _dkm_comm(t, d):
         return None
     dev = t.device.index
     if dev in _COMM:
-        return dev
+        return dev if _COMM[dev] else None
     so = _lib.lib()
     rank, world = d.get_rank(), d.get_world_size()
     buf = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
@@ -84,19 +85,30 @@ def _dkm_comm(t, d):
         _lib.check(so.dkm_allreduce_unique_id(buf), "dkm_allreduce_unique_id")
     obj = [bytes(buf.raw) if rank == 0 else None]
     d.broadcast_object_list(obj, src=0)
-    _lib.check(so.dkm_allreduce_init_rank(obj[0], world, rank, dev),
-               "dkm_allreduce_init_rank")
+    rc = so.dkm_allreduce_init_rank(obj[0], world, rank, dev)
+    # every rank must take the same path: if any rank could not bring the
+    # communicator up, all of them fall back to torch.distributed (RCCL
+    # through the process group) instead of one rank waiting forever
+    import torch
+    ok = torch.tensor([1 if rc == 0 else 0], dtype=torch.int32,
+                      device=t.device)
+    d.all_reduce(ok, op=d.ReduceOp.MIN)
+    if int(ok[0]) == 0:
+        if rc == 0:
+            so.dkm_allreduce_finalize()
+        _COMM[dev] = False
+        return None
     _COMM[dev] = True
     return dev
 
 
 def finalize():
     """Destroy libdkm's RCCL communicators (before the process group)."""
-    if _COMM:
+    if any(_COMM.values()):
         from . import _lib
         _lib.check(_lib.lib().dkm_allreduce_finalize(),
                    "dkm_allreduce_finalize")
-        _COMM.clear()
+    _COMM.clear()
 
 
 def allreduce_sum_(t):
