@@ -1458,8 +1458,15 @@ __global__ void __launch_bounds__(SBB)
   };
 
   typedef float f32x16 __attribute__((ext_vector_type(16)));
+#ifndef DKM_AB_B1_PREFETCH
+#define DKM_AB_B1_PREFETCH 0
+#endif
+  // A/B: prefetch the next tile (and its labels) into the tile registers
+  // as soon as the current one is converted (needs ~64 more VGPRs: pair
+  // with a smaller block, -DDKM_AB_SBB=512)
+  if (DKM_AB_B1_PREFETCH && base + wv * 32 < n) load_tile(base + wv * 32);
   for (int64_t s0 = base + wv * 32; s0 < n; s0 += step) {
-    load_tile(s0);
+    if (!DKM_AB_B1_PREFETCH) load_tile(s0);
     float xx = 0.f;
     bf16x8 xh[NKS];
 #pragma unroll
@@ -1480,6 +1487,7 @@ __global__ void __launch_bounds__(SBB)
       xx = xa + xb;
     }
     const int prv = pv;
+    if (DKM_AB_B1_PREFETCH && s0 + step < n) load_tile(s0 + step);
     const int64_t si = s0 + r;
     float xn;
     const float B2 = bound2_fast(bk, xx, xn);

@@ -4,7 +4,8 @@
 # A/B switches are compile-time only (-DDKM_AB_NO_W32=1, -DDKM_AB_DELTA_POST=1,
 # -DDKM_AB_NO_POST=1, -DDKM_AB_NO_LIST=1, -DDKM_AB_CSR_OLD=1,
 # -DDKM_AB_BLOCKS_PER_CU=n, -DDKM_AB_VERBOSE, -DDKM_AB_SBB=n (k_screen_b1
-# block size)): the product build reads no
+# block size), -DDKM_AB_B1_PREFETCH=1 (k_screen_b1 next-tile prefetch)): the
+# product build reads no
 # environment variable.
 set -e
 cd "$(dirname "$0")"
