@@ -544,6 +544,45 @@ def test_assign_delta_equals_difference_of_partial_sums(mode, d, k):
     assert np.array_equal(a[k * d:], rc - pc)
 
 
+_LONG = {}
+
+
+def _long_fit_reference():
+    """Oracle fit of the long single-product test (computed once)."""
+    if not _LONG:
+        x, _ = make_blobs(n_samples=30000, n_features=64, centers=200,
+                          center_box=(-10, 10), random_state=3)
+        blocks = [x[i:i + 5000] for i in range(0, len(x), 5000)]
+        ref = orc.OracleKMeans(n_clusters=200, max_iter=12, tol=0,
+                               random_state=0)
+        lab = ref.fit(blocks, set_labels=True)
+        _LONG.update(x=x, n_iter=ref.n_iter, labels=lab, centers=ref.centers)
+    return _LONG
+
+
+@pytest.mark.parametrize("refresh", [1000, 8])
+def test_long_fit_single_product_path_matches_oracle(refresh):
+    """12 Lloyd iterations at a shape that runs the single-product screen
+    (k x d sums beyond LDS: d = 64, k = 200) with its label-hinted
+    threshold pass, from the reference's uniform init (heavy migration in
+    the first iterations), with and without the periodic full refresh of
+    the incremental sums: labels bit-exact, centres within 1e-9 relative,
+    same n_iter as the oracle."""
+    import dislib_amd.cluster.kmeans as km_mod
+    g = _long_fit_reference()
+    old = km_mod.REFRESH
+    km_mod.REFRESH = refresh
+    try:
+        ds = _load(g["x"], 5000)
+        km = _km(n_clusters=200, max_iter=12, tol=0, random_state=0)
+        km.fit_predict(ds)
+    finally:
+        km_mod.REFRESH = old
+    assert km.n_iter == g["n_iter"]
+    assert np.array_equal(ds.labels_int32(), g["labels"])
+    _close(km.centers, g["centers"], 1e-9)
+
+
 @pytest.mark.parametrize("refresh", [1, 3, 1000])
 def test_fit_delta_refresh_matches_oracle(refresh):
     import dislib_amd.cluster.kmeans as km_mod
