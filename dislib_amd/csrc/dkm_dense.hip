@@ -1546,15 +1546,25 @@ __global__ void __launch_bounds__(SBB)
         int j0 = 0, j1 = 0, j2 = 0, cnt = 0;
         // scores tested 4 registers at a time (min3 + min + one compare and
         // branch), each register only inside a taken group
-        auto keep = [&](int cb, const f32x16 &accv) {
+        // scores tested 4 registers at a time: the straight-line part (two
+        // v_med3, a min and a compare per group) is interleaved with the
+        // next block's MFMA chain; each register is visited only inside a
+        // taken group (rare)
+        auto test = [&](const f32x16 &accv, bool (&gh)[4]) {
 #pragma unroll
-          for (int g4 = 0; g4 < 16; g4 += 4) {
-            const float mn = fminf(
-                __builtin_amdgcn_fmed3f(accv[g4], accv[g4 + 1], ninf) ,
-                __builtin_amdgcn_fmed3f(accv[g4 + 2], accv[g4 + 3], ninf));
-            if (mn <= T) {
+          for (int q = 0; q < 4; ++q) {
+            const int g4 = 4 * q;
+            gh[q] = fminf(__builtin_amdgcn_fmed3f(accv[g4], accv[g4 + 1], ninf),
+                          __builtin_amdgcn_fmed3f(accv[g4 + 2], accv[g4 + 3],
+                                                  ninf)) <= T;
+          }
+        };
+        auto append = [&](int cb, const f32x16 &accv, const bool (&gh)[4]) {
 #pragma unroll
-              for (int g = g4; g < g4 + 4; ++g) {
+          for (int q = 0; q < 4; ++q) {
+            if (gh[q]) {
+#pragma unroll
+              for (int g = 4 * q; g < 4 * q + 4; ++g) {
                 const float sc = accv[g];
                 if (sc <= T) {
                   const int ci = cb * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
@@ -1593,16 +1603,43 @@ __global__ void __launch_bounds__(SBB)
         {
           f32x16 acc_a, acc_b;
           bf16x8 fa[NKS], fb[NKS];
+          bool ga[4], gb[4];
+          // the block's LDS reads first, then MFMA k of the chain and 4 VALU
+          // of the other block's test
+          auto interleave = [&]() {
+            __builtin_amdgcn_sched_group_barrier(0x100, 4 + NKS, 0);  // DS rd
+#pragma unroll
+            for (int i = 0; i < NKS; ++i) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+              __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
+            }
+          };
           rd(0, fa, acc_a);
           mm(fa, acc_a);
-          for (int cb = 0; cb < nkb; cb += 2) {  // wave-uniform conditions
-            const bool has1 = cb + 1 < nkb, has2 = cb + 2 < nkb;
-            if (has1) rd(cb + 1, fb, acc_b);
-            keep(cb, acc_a);
-            if (has1) mm(fb, acc_b);
-            if (has2) rd(cb + 2, fa, acc_a);
-            if (has1) keep(cb + 1, acc_b);
-            if (has2) mm(fa, acc_a);
+          int cb = 0;
+          for (; cb + 2 < nkb; cb += 2) {  // blocks cb, cb + 1, cb + 2 exist
+            rd(cb + 1, fb, acc_b);
+            test(acc_a, ga);
+            mm(fb, acc_b);
+            interleave();
+            append(cb, acc_a, ga);
+            rd(cb + 2, fa, acc_a);
+            test(acc_b, gb);
+            mm(fa, acc_a);
+            interleave();
+            append(cb + 1, acc_b, gb);
+          }
+          if (cb + 1 < nkb) {  // the last two blocks
+            rd(cb + 1, fb, acc_b);
+            test(acc_a, ga);
+            mm(fb, acc_b);
+            interleave();
+            append(cb, acc_a, ga);
+            test(acc_b, gb);
+            append(cb + 1, acc_b, gb);
+          } else {             // the last block
+            test(acc_a, ga);
+            append(cb, acc_a, ga);
           }
         }
         // the sample's two lanes: union of their kept lists
