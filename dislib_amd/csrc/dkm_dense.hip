@@ -1846,6 +1846,33 @@ __global__ void __launch_bounds__(SBB)
   if (lane == 0 && tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
 }
 
+// One 8-lane share of numpy's pairwise leaf: r_j = sum_i (x[j+8i]-c[j+8i])^2
+// for i < nst (nst <= 16).  Every load is issued before the first use, so an
+// entry costs one memory round trip instead of nst dependent ones.
+template <class TX>
+__device__ __forceinline__ void leaf8_load_x(const TX *xr, int nst,
+                                             double (&xv)[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < nst) xv[i] = (double)xr[8 * i];
+}
+
+__device__ __forceinline__ double leaf8_share(const double (&xv)[16],
+                                              const double *cr, int nst) {
+  double cv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < nst) cv[i] = cr[8 * i];
+  double r = 0.0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < nst) {
+      const double df = xv[i] - cv[i];
+      r = i ? r + df * df : df * df;
+    }
+  return r;
+}
+
 // Two-candidate samples of k_screen_b1: the reference arithmetic (numpy
 // pairwise order, correctly rounded sqrt) on c1 and c2, first index among
 // equal distances.  Labels only.  k_screen_b1 runs only for 8 <= d <= 128
@@ -1876,18 +1903,18 @@ __global__ void __launch_bounds__(BLOCK)
     if (t0 >= cnt) continue;  // wave-uniform
     const int2 *list = v.clist + sg * B1_CAP + t0;
     const int m = min(64, cnt - t0);
+    const int2 own = list[min(lane, m - 1)];  // the batch, one entry a lane
     for (int p = 0; p < m; p += 4) {
       const bool live = p + e < m;
-      const int2 it = list[live ? p + e : 0];
+      const int src = min(p + e, m - 1);
+      const int2 it = make_int2(__shfl(own.x, src, 64), __shfl(own.y, src, 64));
       const int c1 = it.y & 0xffff, c2 = (int)((unsigned)it.y >> 16);
       const int64_t si = base + it.x;
       const TX *xr = X + si * ldx + j;
       const double *cr = C + (int64_t)(cs ? c2 : c1) * d + j;
-      double r = 0.0;
-      for (int i = 0; i < nst; ++i) {
-        const double df = (double)xr[8 * i] - cr[8 * i];
-        r = i ? r + df * df : df * df;
-      }
+      double xv[16];
+      leaf8_load_x(xr, nst, xv);
+      double r = leaf8_share(xv, cr, nst);
       r = r + __shfl_xor(r, 1, 64);
       r = r + __shfl_xor(r, 2, 64);
       r = r + __shfl_xor(r, 4, 64);
@@ -1923,23 +1950,23 @@ __global__ void __launch_bounds__(BLOCK)
     if (t0 >= cnt) continue;  // wave-uniform
     const int4 *list = v.nlist + sg * B1_NCAP + t0;
     const int m = min(64, cnt - t0);
+    const int4 own = list[min(lane, m - 1)];  // the batch, one entry a lane
     for (int q = 0; q < m; q += 8) {
       const bool live = q + e < m;
-      const int4 it = list[live ? q + e : 0];
+      const int src = min(q + e, m - 1);
+      const int4 it = make_int4(__shfl(own.x, src, 64), __shfl(own.y, src, 64),
+                                __shfl(own.z, src, 64), __shfl(own.w, src, 64));
       const int64_t si = base + it.x;
       const TX *xr = X + si * ldx + j;
       const uint32_t pk[3] = {(uint32_t)it.y, (uint32_t)it.z, (uint32_t)it.w};
+      double xv[16];
+      leaf8_load_x(xr, nst, xv);
       double best = INFINITY;
       int bi = -1;
       for (int w = 0; w < 6; ++w) {
         const int c = (int)((pk[w >> 1] >> (16 * (w & 1))) & 0xffffu);
         if (c == 0xffff) break;
-        double r = 0.0;
-        const double *cr = C + (int64_t)c * d + j;
-        for (int i = 0; i < nst; ++i) {
-          const double df = (double)xr[8 * i] - cr[8 * i];
-          r = i ? r + df * df : df * df;
-        }
+        double r = leaf8_share(xv, C + (int64_t)c * d + j, nst);
         r = r + __shfl_xor(r, 1, 64);
         r = r + __shfl_xor(r, 2, 64);
         r = r + __shfl_xor(r, 4, 64);
