@@ -1377,6 +1377,15 @@ __global__ void __launch_bounds__(SBB)
     f32x4 *dst = (f32x4 *)frag;
     for (int e = threadIdx.x; e < nkb * NKS * 64; e += SBB) dst[e] = src[e];
     for (int e = threadIdx.x; e < nkb * 32; e += SBB) cn[e] = v.cn32f[e];
+    // hint == 2: the norm chunks with one slot poisoned (+inf), chunk
+    // (block, half, 4-slot group j, slot t) at ((cb * 2 + h) * 4 + j) * 4 + t
+    if (hint == 2)
+      for (int e = threadIdx.x; e < nkb * 32; e += SBB) {
+        const f32x4 c = ((const f32x4 *)v.cn32f)[e >> 2];
+        f32x4 *dst = (f32x4 *)(cn + nkb * 32) + e;
+        (*dst) = c;
+        (*dst)[e & 3] = INFINITY;
+      }
   }
   const float cm =
       (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
@@ -1541,16 +1550,35 @@ __global__ void __launch_bounds__(SBB)
         const float sp =
             cn[pcb * 32 + 16 * ((pw >> 2) & 1) + (pw & 3) + 4 * (pw >> 3)] + dot;
         const float T = pok ? sp + B2 : -INFINITY;
+        // hint == 2: the lane holding centre p's score (half (p >> 2) & 1)
+        // reads p's norm as +inf in block p >> 5, so its MFMA score for p
+        // never passes the test, and starts its kept list with (s_hat_p, p)
+        // instead: s_hat_p is a score of p from the same bf16 operands,
+        // within the same bound.  Without it every sample's own group took
+        // the append branches once per tile.
+        const bool own_l = hint == 2 && pok && h == ((pw >> 2) & 1);
+        const int own_cb = own_l ? pcb : -1, own_j = pw >> 3;
+        const f32x4 *own_p = (const f32x4 *)(cn + nkb * 32) +
+                             ((pcb * 2 + h) * 4 + own_j) * 4 + (pw & 3);
         // up to 3 kept (score, centre) per lane, in scan order; cnt counts all
-        float q0 = INFINITY, q1 = INFINITY, q2 = INFINITY;
-        int j0 = 0, j1 = 0, j2 = 0, cnt = 0;
+        float q0 = own_l ? sp : INFINITY, q1 = INFINITY, q2 = INFINITY;
+        int j0 = own_l ? p : 0, j1 = 0, j2 = 0, cnt = own_l ? 1 : 0;
         // scores tested 4 registers at a time (min3 + min + one compare and
         // branch), each register only inside a taken group
         // scores tested 4 registers at a time: the straight-line part (two
         // v_med3, a min and a compare per group) is interleaved with the
         // next block's MFMA chain; each register is visited only inside a
         // taken group (rare)
+#ifndef DKM_AB_B1_PROBE
+#define DKM_AB_B1_PROBE 0
+#endif
+        float probe = 0.f;  // A/B timing probes only (results invalid)
         auto test = [&](const f32x16 &accv, bool (&gh)[4]) {
+          if (DKM_AB_B1_PROBE == 2) {
+            probe = fmaxf(probe, accv[0]);
+            gh[0] = gh[1] = gh[2] = gh[3] = false;
+            return;
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int g4 = 4 * q;
@@ -1560,6 +1588,10 @@ __global__ void __launch_bounds__(SBB)
           }
         };
         auto append = [&](int cb, const f32x16 &accv, const bool (&gh)[4]) {
+          if (DKM_AB_B1_PROBE) {
+            probe += (gh[0] | gh[1] | gh[2] | gh[3]) ? 1.f : 0.f;
+            return;
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             if (gh[q]) {
@@ -1586,7 +1618,11 @@ __global__ void __launch_bounds__(SBB)
         // no MFMA waits on an LDS read issued just before it
         auto rd = [&](int cb, bf16x8 (&f)[NKS], f32x16 &accv) {
           const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
-          const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
+          const bool own = cb == own_cb;
+          const f32x4 c0 = *(own && own_j == 0 ? own_p : c4p),
+                      c1 = *(own && own_j == 1 ? own_p : c4p + 1),
+                      c2 = *(own && own_j == 2 ? own_p : c4p + 2),
+                      c3 = *(own && own_j == 3 ? own_p : c4p + 3);
           accv = f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
                         c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
 #pragma unroll
@@ -1641,6 +1677,11 @@ __global__ void __launch_bounds__(SBB)
             test(acc_a, ga);
             append(cb, acc_a, ga);
           }
+        }
+        if (DKM_AB_B1_PROBE) {  // keep the hint as the only candidate
+          cnt = (probe == 12345.f || h != ((pw >> 2) & 1)) ? 0 : 1;
+          q0 = sp;
+          j0 = p;
         }
         // the sample's two lanes: union of their kept lists
         int ocnt, oj0, oj1, oj2;
@@ -2627,7 +2668,12 @@ template <class TX>
 static int launch_screen_b1(const TX *X, int64_t end, int d, int64_t ldx,
                             int k, const WsView &v, int32_t *lab_out,
                             int64_t base, int hint, hipStream_t s, int *nseg) {
-  const size_t lds = b1_frag_bytes(k, d);
+  size_t lds = b1_frag_bytes(k, d);
+  // hint 2: the poisoned norm table (kpad32 x 16 B) fits beside the centres
+  if (hint && lds + (size_t)kpad32(k) * 16 <= B1_LDS_POISON_MAX) {
+    lds += (size_t)kpad32(k) * 16;
+    hint = 2;
+  }
   const int nks = (int)(dpad16(d) / 16);
   const void *kf = nullptr;
 #define DKM_B1(N)                                            \

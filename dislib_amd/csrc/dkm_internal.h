@@ -74,6 +74,7 @@ constexpr int B1_SEGS = 4096;          // >= 256 CUs x 8 waves
 constexpr int B1_CAP = 4096;           // candidate entries per screen wave
 constexpr int B1_NCAP = 1024;          // 3..6-candidate entries per wave
 constexpr size_t B1_LDS_MAX = 150 * 1024;
+constexpr size_t B1_LDS_POISON_MAX = 160 * 1024;  // with the poisoned norms
 
 __host__ __device__ inline int64_t dpad16(int64_t d);
 inline size_t b1_frag_bytes(int64_t k, int64_t d) {
