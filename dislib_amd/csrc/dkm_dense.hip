@@ -1563,29 +1563,30 @@ __global__ void __launch_bounds__(SBB)
         // up to 3 kept (score, centre) per lane, in scan order; cnt counts all
         float q0 = own_l ? sp : INFINITY, q1 = INFINITY, q2 = INFINITY;
         int j0 = own_l ? p : 0, j1 = 0, j2 = 0, cnt = own_l ? 1 : 0;
-        // scores tested 4 registers at a time (min3 + min + one compare and
-        // branch), each register only inside a taken group
-        // scores tested 4 registers at a time: the straight-line part (two
-        // v_med3, a min and a compare per group) is interleaved with the
-        // next block's MFMA chain; each register is visited only inside a
-        // taken group (rare)
+        // each block is tested whole, interleaved with the next block's MFMA
+        // chain: 8 v_med3 pair minima, a v_min3 tree and one compare (13
+        // VALU) and a single branch; the 4-register group tests and the
+        // per-register appends run only inside a taken block, which with the
+        // own centre poisoned means an ambiguous sample (rare).  Per-group
+        // branches (16 VALU, 4 branches a block) ran 28.3 against 26.6 ms
+        // per C3 step (profiles/r02/ab_m3/).
 #ifndef DKM_AB_B1_PROBE
 #define DKM_AB_B1_PROBE 0
 #endif
         float probe = 0.f;  // A/B timing probes only (results invalid)
-        auto test = [&](const f32x16 &accv, bool (&gh)[4]) {
+        auto test_blk = [&](const f32x16 &accv, float (&m)[8], bool &any) {
           if (DKM_AB_B1_PROBE == 2) {
             probe = fmaxf(probe, accv[0]);
-            gh[0] = gh[1] = gh[2] = gh[3] = false;
+            any = false;
             return;
           }
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int g4 = 4 * q;
-            gh[q] = fminf(__builtin_amdgcn_fmed3f(accv[g4], accv[g4 + 1], ninf),
-                          __builtin_amdgcn_fmed3f(accv[g4 + 2], accv[g4 + 3],
-                                                  ninf)) <= T;
-          }
+          for (int i = 0; i < 8; ++i)
+            m[i] = __builtin_amdgcn_fmed3f(accv[2 * i], accv[2 * i + 1], ninf);
+          const float a = fminf(fminf(m[0], m[1]), m[2]);
+          const float b = fminf(fminf(m[3], m[4]), m[5]);
+          const float c = fminf(fminf(m[6], m[7]), a);
+          any = fminf(b, c) <= T;
         };
         auto append = [&](int cb, const f32x16 &accv, const bool (&gh)[4]) {
           if (DKM_AB_B1_PROBE) {
@@ -1636,12 +1637,21 @@ __global__ void __launch_bounds__(SBB)
             accv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[ks], xh[ks], accv,
                                                            0, 0, 0);
         };
+        auto append_blk = [&](int cb, const f32x16 &accv, const float (&m)[8],
+                              bool any) {
+          if (any) {
+            bool gh[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              gh[q] = __builtin_amdgcn_fmed3f(m[2 * q], m[2 * q + 1], ninf) <= T;
+            append(cb, accv, gh);
+          }
+        };
         {
           f32x16 acc_a, acc_b;
           bf16x8 fa[NKS], fb[NKS];
-          bool ga[4], gb[4];
-          // the block's LDS reads first, then MFMA k of the chain and 4 VALU
-          // of the other block's test
+          float ma[8], mb[8];
+          bool ga, gb;
           auto interleave = [&]() {
             __builtin_amdgcn_sched_group_barrier(0x100, 4 + NKS, 0);  // DS rd
 #pragma unroll
@@ -1653,29 +1663,29 @@ __global__ void __launch_bounds__(SBB)
           rd(0, fa, acc_a);
           mm(fa, acc_a);
           int cb = 0;
-          for (; cb + 2 < nkb; cb += 2) {  // blocks cb, cb + 1, cb + 2 exist
+          for (; cb + 2 < nkb; cb += 2) {
             rd(cb + 1, fb, acc_b);
-            test(acc_a, ga);
+            test_blk(acc_a, ma, ga);
             mm(fb, acc_b);
             interleave();
-            append(cb, acc_a, ga);
+            append_blk(cb, acc_a, ma, ga);
             rd(cb + 2, fa, acc_a);
-            test(acc_b, gb);
+            test_blk(acc_b, mb, gb);
             mm(fa, acc_a);
             interleave();
-            append(cb + 1, acc_b, gb);
+            append_blk(cb + 1, acc_b, mb, gb);
           }
-          if (cb + 1 < nkb) {  // the last two blocks
+          if (cb + 1 < nkb) {
             rd(cb + 1, fb, acc_b);
-            test(acc_a, ga);
+            test_blk(acc_a, ma, ga);
             mm(fb, acc_b);
             interleave();
-            append(cb, acc_a, ga);
-            test(acc_b, gb);
-            append(cb + 1, acc_b, gb);
-          } else {             // the last block
-            test(acc_a, ga);
-            append(cb, acc_a, ga);
+            append_blk(cb, acc_a, ma, ga);
+            test_blk(acc_b, mb, gb);
+            append_blk(cb + 1, acc_b, mb, gb);
+          } else {
+            test_blk(acc_a, ma, ga);
+            append_blk(cb, acc_a, ma, ga);
           }
         }
         if (DKM_AB_B1_PROBE) {  // keep the hint as the only candidate
