@@ -17,7 +17,11 @@ events on its stream), a CPU baseline (the oracle on this host, rank 0,
 N=1 only, bounded sample), the fit_predict variant (labels written), and
 under "extra_configs" the other single-GPU BASELINE configs measured the
 same way in the same run: configs[2]'s per-GPU shard (125M x 64, k=1000,
-the north-star target) and configs[3] (10M x 1024, k=4096, fp64; MFMA).
+the north-star target), configs[3] (10M x 1024, k=4096, fp64 and fp32;
+MFMA) and configs[4] (CSR 10M x 10k, 10 entries per row, k=256: fit and
+predict).  Every line also carries the whole-fit figure:
+the W + K iterations from the initial centres, iteration 0 included,
+tol = 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--only-headline]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -37,6 +41,7 @@ METRIC = "KMeans samples·iters/sec at 1/2/4/8 GPUs + % of HBM/MFMA roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6        # fp64 vector = matrix
+L2_PEAK_TBS = 34.5             # aggregate L2 (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -82,70 +87,94 @@ def cpu_share():
     return max(1, min(share, aff)), aff
 
 
-def cpu_baseline(d, k, target_s, centers, n_blobs, share):
+def cpu_baseline(d, k, target_s, centers, n_blobs, share, csr_nnz=0):
     """One Lloyd iteration's partial sums on a bounded sample of the same
     workload, one Subset per task over a process pool of `share` = (cores,
     machine threads) workers (BLAS threads 1), then the arity-50 merge and
     the centre update -- the reference's task graph (base.py:113-147) run
-    by the vectorised oracle."""
+    by the vectorised oracle.  csr_nnz > 0: CSR rows of the C5 generator
+    (the oracle's sklearn-order sparse distances, base.py:169)."""
     cores, machine = share
     os.environ["OMP_NUM_THREADS"] = "1"        # BLAS threads of the workers
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
     import multiprocessing as mp
     from oracle import kmeans_oracle as orc
+    sparse = csr_nnz > 0
     # probe: single-core rate on a small block (smaller for large k*d)
-    probe = int(max(16, min(4000, 3e8 / (k * d))))
-    xb, _ = orc.make_blobs_rows(0, probe, d, n_blobs, seed=0)
+    probe = 500 if sparse else int(max(16, min(4000, 3e8 / (k * d))))
+    xb = _cpu_gen((0, probe, d, n_blobs, csr_nnz))
     t0 = time.perf_counter()
-    orc.partial_sum(xb, centers)
+    orc.partial_sum(xb, centers, sparse=sparse)
     rate1 = probe / (time.perf_counter() - t0)
-    rows_per_task = int(max(16, min(25_000, rate1 * 0.5)))
+    rows_per_task = int(max(16, min(2000 if sparse else 25_000,
+                                    rate1 * 0.5)))
     n_tasks = max(cores, int(rate1 * cores * target_s / rows_per_task))
-    tasks = [(i * rows_per_task, rows_per_task, d, n_blobs)
+    tasks = [(i * rows_per_task, rows_per_task, d, n_blobs, csr_nnz)
              for i in range(n_tasks)]
     ctx = mp.get_context("fork")
     with ctx.Pool(cores) as pool:
         pool.map(_cpu_gen, tasks[:cores])          # warm the workers
         blocks = pool.map(_cpu_gen, tasks)
         t0 = time.perf_counter()
-        parts = pool.starmap(_cpu_task, [(b, centers) for b in blocks])
+        parts = pool.starmap(_cpu_task, [(b, centers, sparse)
+                                         for b in blocks])
         root = orc.merge_tree(parts, 50)
-        orc.recompute_centers(centers.copy(), root)
+        orc.recompute_centers(centers.copy(), root, sparse=sparse)
         el = time.perf_counter() - t0
     n = n_tasks * rows_per_task
-    # faithful per-sample-loop variant (the reference's own cost model)
-    m = int(max(4, min(2000, rate1 * 0.02)))
-    xs, _ = orc.make_blobs_rows(0, m, d, n_blobs, seed=0)
-    t0 = time.perf_counter()
-    for s in xs:
-        np.argmin(orc.vec_matrix_euclid(s, centers))
-    faithful = m / (time.perf_counter() - t0)
-    return {"value": n / el, "unit": "samples·iters/s", "cores": cores,
-            "kind": "port",
-            "sample": "%d rows (%d Subsets of %d) of the same make_blobs "
-                      "workload, one Lloyd iteration (distances+argmin+"
-                      "sums+arity-50 merge), vectorised numpy oracle, one "
-                      "process per core of this job's CPU share, BLAS "
-                      "threads 1" % (n, n_tasks, rows_per_task),
-            "seconds": el,
-            "per_core": n / el / cores,
-            "machine_threads": machine,
-            "note": "cores = the CPU share the GPU box grants one GPU's job "
-                    "(OMP_NUM_THREADS); the oracle scales linearly over "
-                    "Subsets, so per_core x machine_threads bounds a "
-                    "whole-machine run",
-            "faithful_per_sample_loop_1core": faithful}
+    out = {"value": n / el, "unit": "samples·iters/s", "cores": cores,
+           "kind": "port",
+           "sample": "%d rows (%d Subsets of %d) of the same %s workload, "
+                     "one Lloyd iteration (distances+argmin+sums+arity-50 "
+                     "merge), vectorised numpy oracle, one process per core "
+                     "of this job's CPU share, BLAS threads 1" %
+                     (n, n_tasks, rows_per_task,
+                      "CSR" if sparse else "make_blobs"),
+           "seconds": el,
+           "per_core": n / el / cores,
+           "machine_threads": machine,
+           "note": "cores = the CPU share the GPU box grants one GPU's job "
+                   "(OMP_NUM_THREADS = 16; the harness caps a job's worker "
+                   "pools at that share, not the %d-thread affinity mask); "
+                   "the oracle scales linearly over Subsets, so per_core x "
+                   "machine_threads bounds a whole-machine run" % machine}
+    if not sparse:
+        # faithful per-sample-loop variant (the reference's own cost model)
+        m = int(max(4, min(2000, rate1 * 0.02)))
+        xs = _cpu_gen((0, m, d, n_blobs, 0))
+        t0 = time.perf_counter()
+        for row in xs:
+            np.argmin(orc.vec_matrix_euclid(row, centers))
+        out["faithful_per_sample_loop_1core"] = \
+            m / (time.perf_counter() - t0)
+    return out
+
+
+def csr_rows(row0, n, d, nnz, seed=0):
+    """C5 rows [row0, row0 + n): nnz strictly increasing random columns of
+    d per row, values U(0, 1); counter-based per row block so that any
+    range regenerates identically (host numpy, scipy CSR)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng([seed, row0, n])
+    gap = max(1, d // nnz - 1)
+    cols = np.cumsum(rng.integers(1, gap + 1, (n, nnz)), axis=1) - 1
+    indptr = np.arange(0, n * nnz + 1, nnz, dtype=np.int64)
+    data = rng.random(n * nnz)
+    return sp.csr_matrix((data, cols.reshape(-1).astype(np.int32), indptr),
+                         shape=(n, d))
 
 
 def _cpu_gen(args):
     from oracle import kmeans_oracle as orc
-    row0, n, d, nb = args
+    row0, n, d, nb, nnz = args
+    if nnz:
+        return csr_rows(row0, n, d, nnz, seed=1)
     return orc.make_blobs_rows(row0, n, d, nb, seed=0)[0]
 
 
-def _cpu_task(block, centers):
+def _cpu_task(block, centers, sparse=False):
     from oracle import kmeans_oracle as orc
-    _, s, c = orc.partial_sum(block, centers)
+    _, s, c = orc.partial_sum(block, centers, sparse=sparse)
     return (s, c)
 
 
@@ -153,24 +182,40 @@ def _cpu_task(block, centers):
 # one configuration on the GPU(s)
 # ---------------------------------------------------------------------------
 def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
-               mode, labels, n_blobs=None, f32=False):
+               mode, labels, n_blobs=None, f32=False, csr_nnz=0):
+    """One configuration: a fresh fit state, W warmup iterations, then
+    exactly K timed iterations (barrier + synchronize on both sides).
+    The fit starts at iteration 0 (initial centres, the most expensive
+    step), so warmup + timed iterations are one whole fit of W + K
+    iterations with tol = 0: its wall time (barrier waits excluded) is the
+    SURVEY 8(d) whole-loop figure, from the initialised centres through the
+    last convergence decision."""
     from dislib_amd import _device, _shard
     from dislib_amd.cluster.kmeans import _Lloyd, _init_centers
     from dislib_amd.data import Dataset, Subset
     n_blobs = n_blobs or k
-    X = torch.empty((n, d), dtype=torch.float64, device=dev)
-    # global rows [rank*n, (rank+1)*n): the ranks shard one dataset
-    _device.make_blobs(X, rank * n, n_blobs, seed=0, box=10.0, std=1.0)
-    if f32:                  # fp32 samples: fp64 distances, fp32 sums
-        X = X.to(torch.float32)
-        torch.cuda.empty_cache()
-    ds = Dataset(n_features=d)
+    if csr_nnz:
+        # global rows [rank*n, (rank+1)*n): the ranks shard one dataset
+        X = csr_rows(rank * n, n, d, csr_nnz, seed=1)
+        C0 = _init_centers(d, True, k, 0).toarray()
+    else:
+        X = torch.empty((n, d), dtype=torch.float64, device=dev)
+        _device.make_blobs(X, rank * n, n_blobs, seed=0, box=10.0, std=1.0)
+        if f32:              # fp32 samples: fp64 distances, fp32 sums
+            X = X.to(torch.float32)
+            torch.cuda.empty_cache()
+        C0 = _init_centers(d, False, k, 0)
+    ds = Dataset(n_features=d, sparse=bool(csr_nnz))
     for i in range(0, n, subset):
         ds.append(Subset(X[i:i + subset]))
-    st = _Lloyd(ds, _init_centers(d, False, k, 0), 0.0, labels, mode, dev)
+    ds._device_data(dev)                  # resident before the fit starts
+    st = _Lloyd(ds, C0, 0.0, labels, mode, dev)
     torch.cuda.synchronize()
+    tf = time.perf_counter()
     for _ in range(warmup):
         st.step()
+    torch.cuda.synchronize()
+    warm_s = time.perf_counter() - tf
     ev = [(torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     if world > 1:
@@ -189,16 +234,41 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
         dist.barrier()
     el = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    pred_ms = None
+    if csr_nnz:                       # predict on the final centres
+        from dislib_amd import _lib
+        lab = torch.empty(st.dd.n, dtype=torch.int32, device=dev)
+        _device.predict(st.dd, st.C, st.ws, lab, _lib.MODE_AUTO)
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        for _ in range(3):
+            _device.predict(st.dd, st.C, st.ws, lab, _lib.MODE_AUTO)
+        torch.cuda.synchronize()
+        pred_ms = (time.perf_counter() - tp) / 3 * 1e3
+        del lab
     if world > 1:
-        t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([el, kern_ms, warm_s], dtype=torch.float64,
+                         device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, kern_ms = float(t[0]), float(t[1])
+        el, kern_ms, warm_s = float(t[0]), float(t[1]), float(t[2])
+    info = _shard.comm_info(dev.index) if world > 1 else None
     out = {"el": el, "kern_ms": kern_ms, "rechecked": st.rechecked(),
-           "collective": ("libdkm-rccl" if any(_shard._COMM.values()) else
-                          "torch.distributed") if world > 1 else "none"}
+           "fit_s": warm_s + el, "fit_iters": warmup + steps,
+           "pred_ms": pred_ms,
+           "collective": ("libdkm-rccl" if info else "torch.distributed")
+           if world > 1 else "none",
+           "rccl_ranks": info[0] if info else None}
     del st, ds, X
     torch.cuda.empty_cache()
     return out
+
+
+def fit_fields(r, n, world):
+    """The whole-fit figure of a run: W + K iterations from
+    the initial centres, tol = 0."""
+    return {"fit_iters": r["fit_iters"], "fit_s": r["fit_s"],
+            "fit_ms_per_iter": r["fit_s"] / r["fit_iters"] * 1e3,
+            "fit_value": n * world * r["fit_iters"] / r["fit_s"]}
 
 
 def screen_products(k, d):
@@ -211,14 +281,31 @@ def screen_products(k, d):
     return 3 if frags + (k * lds_stride + k) * 8 <= 80 * 1024 else 1
 
 
-def roofline(n, d, k, r, labels, es=8):
+def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
     """Roofline of the assignment call (the dominant kernels).  Small d:
     HBM-bound, algorithmic bytes = X read (8 d) + labels (delta path:
     previous label read 4 B + label write 4 B).  d > 128: MFMA-bound, the
     executed MFMA flops of the single-product GEMM screen (2 k d per sample
-    over the padded tiles) against the dense bf16 peak."""
+    over the padded tiles) against the dense bf16 peak.  CSR (C5): the HBM
+    bytes of the rows (12 B per stored entry + 8 B of indptr) and labels;
+    its real limit is the gather of fp32 centre columns from L2 (4 B per
+    stored entry and centre), reported beside it."""
     sec = r["kern_ms"] * 1e-3
-    if d <= 128:
+    if csr_nnz:
+        b = n * (12 * csr_nnz + 8 + 8)
+        g = n * csr_nnz * k * 4
+        out = {"bound": "hbm", "achieved": b / sec / 1e9,
+               "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": b / sec / 1e9 / HBM_PEAK_GBS,
+               "bytes_per_sample": 12 * csr_nnz + 16,
+               "kernel": "dkm_assign_delta_csr / dkm_partial_sum_csr (slice "
+                         "screen + merge + resolve)",
+               "kernel_ms": r["kern_ms"],
+               "l2_gather": {"bytes_per_sample": csr_nnz * k * 4,
+                             "achieved_tbs": g / sec / 1e12,
+                             "peak_tbs": L2_PEAK_TBS,
+                             "frac": g / sec / 1e12 / L2_PEAK_TBS}}
+    elif d <= 128:
         b = n * (8 * d + 8)
         out = {"bound": "hbm", "achieved": b / sec / 1e9,
                "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -258,17 +345,21 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    sc = a.extras_scale
     extras = [] if a.only_headline else [
-        # (name, n, d, k, subset, steps, warmup, fp32 samples)
+        # (name, n, d, k, subset, steps, warmup, fp32 samples, csr nnz/row)
         ("KMeans k=1000 on 125M x 64 fp64 dense per GPU (BASELINE "
          "configs[2] per-GPU shard; north-star target)",
-         125_000_000, 64, 1000, 1_000_000, 10, 2, False),
+         125_000_000, 64, 1000, 1_000_000, 8, 2, False, 0),
         ("KMeans k=4096 on 10M x 1024 fp64 dense per GPU (BASELINE "
-         "configs[3], MFMA-bound)", 10_000_000, 1024, 4096, 1_000_000, 5, 3,
-         False),
+         "configs[3], MFMA-bound)", 10_000_000, 1024, 4096, 1_000_000, 4, 2,
+         False, 0),
         ("KMeans k=4096 on 10M x 1024 fp32 dense per GPU (BASELINE "
          "configs[3], fp32 variant reported separately)", 10_000_000, 1024,
-         4096, 1_000_000, 5, 3, True),
+         4096, 1_000_000, 4, 2, True, 0),
+        ("KMeans k=256 on sparse CSR 10M x 10k at 0.1% density per GPU "
+         "(BASELINE configs[4], fit + predict)", 10_000_000, 10_000, 256,
+         1_000_000, 4, 1, False, 10),
     ]
 
     # CPU baselines first, before anything touches the GPU: their worker
@@ -280,14 +371,18 @@ def main():
         share = cpu_share()       # before the workers' BLAS settings below
         cpu["head"] = cpu_baseline(a.d, a.k, a.cpu_seconds,
                                    _ic(a.d, False, a.k, 0), a.k, share)
-        for i, (_, n, d, k, *_r, f32) in enumerate(extras):
+        for i, (_, n, d, k, *_r, f32, nnz) in enumerate(extras):
             if f32:
                 continue          # the fp64 line's baseline covers the shape
             cpu[i] = cpu_baseline(d, k, a.cpu_seconds / 2,
-                                  _ic(d, False, k, 0), k, share)
+                                  _ic(d, bool(nnz), k, 0), k, share,
+                                  csr_nnz=nnz)
 
     import torch
     import torch.distributed as dist
+
+    from dislib_amd import _lib
+    build_flags = int(_lib.load().dkm_build_flags())
     # one rank per GPU; a rehearsal with more ranks than GPUs (gloo) shares
     ndev = max(1, torch.cuda.device_count())
     torch.cuda.set_device(local % ndev)
@@ -298,26 +393,46 @@ def main():
         else:
             dist.init_process_group(a.backend)
 
+    def check_collective(r):
+        # under nccl the Lloyd loop's all-reduce must be libdkm's RCCL
+        # communicator over all ranks, never the silent torch fallback
+        if world > 1 and a.backend == "nccl" and (
+                r["collective"] != "libdkm-rccl" or r["rccl_ranks"] != world):
+            sys.stderr.write("bench: collective %s over %s ranks, expected "
+                             "libdkm-rccl over %d\n" % (
+                                 r["collective"], r["rccl_ranks"], world))
+            raise SystemExit(3)
+
     r = run_config(torch, dist, dev, rank, world, a.n, a.d, a.k, a.subset,
                    a.steps, a.warmup, a.mode, a.labels)
+    check_collective(r)
     fp = None
     if not a.only_headline and not a.labels:
         fp = run_config(torch, dist, dev, rank, world, a.n, a.d, a.k,
                         a.subset, a.steps, a.warmup, a.mode, True)
     ex = []
-    for i, (name, n, d, k, sub, steps, warm, f32) in enumerate(extras):
-        if a.extras_scale != 1.0:
-            n = max(sub, int(n * a.extras_scale) // sub * sub)
+    for i, (name, n, d, k, sub, steps, warm, f32, nnz) in enumerate(extras):
+        if sc != 1.0:
+            n = max(sub, int(n * sc) // sub * sub)
             name += " [scaled to %d rows per GPU]" % n
         rr = run_config(torch, dist, dev, rank, world, n, d, k, sub, steps,
-                        warm, a.mode, False, f32=f32)
+                        warm, a.mode, False, f32=f32, csr_nnz=nnz)
+        check_collective(rr)
         e = {"workload": name, "n_per_gpu": n, "d": d, "k": k,
              "dtype": "f32 samples (f64 distances)" if f32 else "f64",
              "value": n * world * steps / rr["el"],
              "unit": "samples·iters/s", "ms_per_step": rr["el"] / steps * 1e3,
              "steps": steps, "warmup": warm,
-             "roofline": roofline(n, d, k, rr, False, 4 if f32 else 8),
+             "roofline": roofline(n, d, k, rr, False, 4 if f32 else 8,
+                                  csr_nnz=nnz),
              "rechecked_samples": rr["rechecked"]}
+        e.update(fit_fields(rr, n, world))
+        if nnz:
+            e["nnz_per_row"] = nnz
+            e["predict_ms"] = rr["pred_ms"]
+            e["predict_samples_per_s"] = n / (rr["pred_ms"] * 1e-3)
+        if world > 1:
+            e["rccl_ranks"] = rr["rccl_ranks"]
         if i in cpu:
             cpu[i]["gpu_over_cpu"] = e["value"] / cpu[i]["value"]
             e["cpu_baseline"] = cpu[i]
@@ -366,6 +481,11 @@ def main():
         "rechecked_samples": r["rechecked"],
         "collective": r["collective"],
     }
+    out.update(fit_fields(r, a.n, world))
+    if world > 1:
+        out["rccl_ranks"] = r["rccl_ranks"]
+    if build_flags:
+        out["timing_only_build"] = build_flags   # A/B probe library
     if fp is not None:
         out["fit_predict"] = {
             "value": a.n * world * a.steps / fp["el"],

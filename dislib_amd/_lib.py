@@ -69,6 +69,11 @@ SIGNATURES = {
     "dkm_allreduce_init": (_i32, [_i32, ctypes.POINTER(_i32)]),
     "dkm_allreduce_sum_f64": (_i32, [_p, _i64, _i32, _p]),
     "dkm_allreduce_finalize": (_i32, []),
+    "dkm_allreduce_finalize_device": (_i32, [_i32]),
+    "dkm_allreduce_available": (_i32, []),
+    "dkm_allreduce_comm_info": (_i32, [_i32, ctypes.POINTER(_i32),
+                                       ctypes.POINTER(_i32)]),
+    "dkm_build_flags": (_i32, []),
     # host-side loaders (no GPU)
     "dkm_libsvm_count": (_i32, [_p, _i64, _i32, _p]),
     "dkm_libsvm_parse": (_i32, [_p, _i64, _i32, _p, _p, _p, _p, _p]),

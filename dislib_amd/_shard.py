@@ -69,8 +69,17 @@ _COMM = {}   # device index -> True once libdkm's RCCL communicator is up,
 def _dkm_comm(t, d):
     """libdkm's RCCL communicator for ``t``'s device, brought up on first
     use (every rank reaches its first all-reduce together).  None when the
-    group is not ``nccl`` or ``t`` is not a GPU tensor."""
+    group is not ``nccl`` or ``t`` is not a GPU tensor.
+
+    The ranks agree on the path BEFORE the collective ncclCommInitRank
+    (which blocks until every rank has joined): each rank checks that
+    librccl loads, rank 0 also creates the id, and one MIN all-reduce of
+    those flags decides for all.  Only after a successful init do the ranks
+    agree once more; a rank whose init failed then destroys nothing but its
+    own device's communicator."""
     import ctypes
+
+    import torch
 
     from . import _lib
     if d.get_backend() != "nccl" or not t.is_cuda:
@@ -80,26 +89,45 @@ def _dkm_comm(t, d):
         return dev if _COMM[dev] else None
     so = _lib.lib()
     rank, world = d.get_rank(), d.get_world_size()
+
+    def all_ok(flag):
+        f = torch.tensor([1 if flag else 0], dtype=torch.int32,
+                         device=t.device)
+        d.all_reduce(f, op=d.ReduceOp.MIN)
+        return int(f[0]) == 1
+
     buf = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
-    if rank == 0:
-        _lib.check(so.dkm_allreduce_unique_id(buf), "dkm_allreduce_unique_id")
+    ok = so.dkm_allreduce_available() == 0
+    if rank == 0 and ok:
+        ok = so.dkm_allreduce_unique_id(buf) == 0
+    if not all_ok(ok):
+        _COMM[dev] = False
+        return None
     obj = [bytes(buf.raw) if rank == 0 else None]
     d.broadcast_object_list(obj, src=0)
     rc = so.dkm_allreduce_init_rank(obj[0], world, rank, dev)
-    # every rank must take the same path: if any rank could not bring the
-    # communicator up, all of them fall back to torch.distributed (RCCL
-    # through the process group) instead of one rank waiting forever
-    import torch
-    ok = torch.tensor([1 if rc == 0 else 0], dtype=torch.int32,
-                      device=t.device)
-    d.all_reduce(ok, op=d.ReduceOp.MIN)
-    if int(ok[0]) == 0:
-        if rc == 0:
-            so.dkm_allreduce_finalize()
+    if not all_ok(rc == 0):
+        so.dkm_allreduce_finalize_device(dev)
         _COMM[dev] = False
         return None
     _COMM[dev] = True
     return dev
+
+
+def comm_info(device):
+    """(ranks, rank) of libdkm's RCCL communicator on ``device``, or None
+    when it has none (single process, gloo, or the torch.distributed
+    fallback)."""
+    import ctypes
+
+    from . import _lib
+    if not _COMM.get(device):
+        return None
+    n, r = ctypes.c_int(0), ctypes.c_int(0)
+    _lib.check(_lib.lib().dkm_allreduce_comm_info(device, ctypes.byref(n),
+                                                  ctypes.byref(r)),
+               "dkm_allreduce_comm_info")
+    return n.value, r.value
 
 
 def finalize():

@@ -1,0 +1,660 @@
+// dkm_b2.hip -- single-product screen with the centres on the lanes
+// (k_screen_b2): the threshold pass of the k x d > LDS-sums shapes (C3:
+// 125M x 64, k = 1000 per GPU), replacing k_screen_b1's (dkm_dense.hip).
+//
+// The reference step it serves is `_partial_sum`'s distance + argmin
+// (dislib cluster/kmeans/base.py:171-173, `_vec_matrix_euclid` :204-205).
+// Labels stay bit-exact: the screen only decides a sample when the bound
+// proves the winner; everything else goes to the exact re-check kernels.
+//
+// Why the transpose.  k_screen_b1 multiplies A = centres (rows) by B =
+// samples (columns), so a lane holds one sample and 16 centres, and every
+// 32-centre block needs 16 norms per lane from LDS (4 ds_read_b128, as many
+// LDS cycles as the block's 4 fragment reads).  At 3 waves per SIMD that is
+// 2 ds_read_b128 per MFMA: the LDS array (256 B/clk/CU) is saturated at the
+// MFMA rate.  Here A = samples and B = centres: lane l holds centre
+// cb*32 + (l & 31) and 16 samples (rows (g & 3) + 8 (g >> 2) + 4h).  The
+// accumulator starts from -T (T = the sample's threshold, a per-tile
+// constant block), so the block test is
+//     min_g (dot_gj - T_g) <= -|c_j|^2
+// with one per-lane norm (ds_read_b32): 18 LDS cycles per block instead
+// of 32, no per-block address selects.
+//
+// Threshold (label hint p = the sample's incoming label, as in b1):
+//   s_hat_p = |c_p|^2 + x.(-2c_p)h from the same bf16 operands (an MFMA
+//   "own block" whose columns are the tile's hinted centres: its diagonal),
+//   T = s_hat_p + 2B.  A centre with s_j > T cannot win or tie.
+// Own exclusion: the hinted centres P = {p_i} always pass.  A column whose
+// centre is in P is masked (per-column bit mask over blocks, one v_bfe +
+// one v_and_or per block) for every row of the tile, and the pairs
+// (i, p_c), p_c in P, p_c != p_i, are tested once in the own block instead
+// (duplicate hints: only the first column of a centre is tested).  So every
+// (sample, centre) pair is tested exactly once, p_i itself by s_hat_p.
+// Kept pairs (rare) go to a per-wave LDS list of B2_ENT entries per sample;
+// the decision (unique / two / many / re-check) is b1's.
+//
+// Bound: B2t = 2 (1.02 2^-8 + (32 NKS + 16) 2^-23) mag: bf16 rounding of x
+// and -2c, the fp32 MFMA chain (now over |T| + sum |x c|, <= 2.04 mag), the
+// ŝ_p chain, and the few roundings of (acc + T) + |c|^2 -- each <= 2^-23 of
+// a magnitude <= 2.04 mag.  The top-3 fallback keeps b1's packed bound.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "dkm_internal.h"
+#include "dkm_screen.h"
+
+namespace dkm {
+
+#ifndef DKM_AB_SB2
+#define DKM_AB_SB2 768
+#endif
+constexpr int SB2 = DKM_AB_SB2;
+constexpr uint32_t PACK2 = 9, PACK2_MASK = (1u << PACK2) - 1;
+constexpr int B2_ENT = 3;    // kept (score, centre) per sample besides p
+constexpr int B2_RTHR = 4;   // over-full samples a wave tolerates per tile
+// per-wave LDS scratch: -T[32], hint[32], count[32], entries[32][B2_ENT],
+// then 32 x nkw own-mask words
+constexpr int B2_SCR_FIXED = 3 * 128 + 32 * B2_ENT * 8;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <class TX, int NKS, bool W1>
+__global__ void __launch_bounds__(SB2)
+    k_screen_b2(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
+                WsView v, int32_t *__restrict__ lab_out, int64_t base,
+                int delta, int hint) {
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  constexpr int GB = 1 << (PACK2 - 4);  // 32-centre blocks per top-3 group
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nkb = (int)(kpad32(k) / 32);
+  // W1: one own-mask word per column (k <= 1024), held in a register
+  const int nkw = W1 ? 1 : (nkb + 31) >> 5;
+  char *frag = (char *)smem;                                // nkb x NKS KB
+  float *cn = (float *)(frag + (int64_t)nkb * NKS * 1024);  // b1 order
+  float *ncn = cn + nkb * 32;                               // -|c|^2, plain
+  char *scr0 = (char *)(ncn + nkb * 32);
+  {
+    const f32x4 *src = (const f32x4 *)v.b1frag;
+    f32x4 *dst = (f32x4 *)frag;
+    for (int e = threadIdx.x; e < nkb * NKS * 64; e += SB2) dst[e] = src[e];
+    for (int e = threadIdx.x; e < nkb * 32; e += SB2) {
+      cn[e] = v.cn32f[e];
+      // padding centres: -2^100 (never passes a sane threshold)
+      ncn[e] = e < k ? -v.cn32[e] : -0x1.0p100f;
+    }
+  }
+  const float cm =
+      (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
+  // top-3 fallback: b1's packed single-product bound
+  const float rel = 1.02f * 0x1.0p-8f + (16.0f * NKS + 2.0f) * 0x1.0p-23f;
+  BoundK bk = bound_consts<P_F32>(d, cm);
+  bk.k_mag = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(
+      2.0f * (2.0f * rel + 0x1.0p-23f * (float)(1u << PACK2)) * 1.0001f)));
+  // threshold pass: no packing, the chain over |T| + sum |x c| (see top)
+  const float relt = 1.02f * 0x1.0p-8f + (32.0f * NKS + 16.0f) * 0x1.0p-23f;
+  BoundK bkt = bk;
+  bkt.k_mag = __int_as_float(__builtin_amdgcn_readfirstlane(
+      __float_as_int(2.0f * (2.0f * relt) * 1.0001f)));
+  const float ninf = __uint_as_float(opaque_u32(0xff800000u));
+  const uint32_t vmask = opaque_u32(~PACK2_MASK);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t wv = (int64_t)blockIdx.x * (SB2 / 64) + wid;
+  const int64_t step = (int64_t)gridDim.x * (SB2 / 64) * 32;
+  char *scr = scr0 + (int64_t)wid * (B2_SCR_FIXED + 128 * nkw);
+  float *s_tn = (float *)scr;              // -T per sample
+  int *s_hp = (int *)(scr + 128);          // hint per sample (-1: none)
+  int *s_cnt = (int *)(scr + 256);         // kept entries appended
+  int2 *s_ent = (int2 *)(scr + 384);       // (score bits, centre)
+  uint32_t *s_om = (uint32_t *)(scr + B2_SCR_FIXED);  // [word][column]
+  int2 *wl = v.tlist + wv * TL_CAP;  // >= 3 candidates
+  int2 *cl = v.clist + wv * B1_CAP;  // 2 candidates
+  int4 *nl = v.nlist + wv * B1_NCAP; // 3..6 candidates
+  int nl_cnt = 0;
+  const bool listing = wv < TL_SEGS && wv < B1_SEGS;
+  int tl_cnt = 0, cl_cnt = 0, tl_over = 0;
+  uint32_t t_tiles = 0, t_done = 0;  // threshold passes run / accepted
+
+  double tile[NKS][8];
+  int pv = -1;
+  const uint32_t lane_off = (uint32_t)(r * ldx * (int64_t)sizeof(TX)) +
+                            (uint32_t)(8 * h * sizeof(TX));
+  auto load_tile = [&](int64_t s0) {
+    const int64_t rows = std::max<int64_t>(0, n - s0);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(X + std::min(s0, n) * ldx), 0,
+        (int)std::min<int64_t>(rows * ldx * (int64_t)sizeof(TX), 0x7fffffff),
+        0x00020000);
+    if (delta || hint) {
+      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(lab_out + std::min(s0, n)), 0,
+          (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
+      pv = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
+    }
+    // all of the tile's loads unconditionally (one wait covers them); rows
+    // past n read 0 (num_records), features past d are zeroed below
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int o = 16 * ks * (int)sizeof(TX);
+      if constexpr (sizeof(TX) == 8) {
+#pragma unroll
+        for (int p4 = 0; p4 < 4; ++p4) {
+          const double2 v2 = __builtin_bit_cast(
+              double2, __builtin_amdgcn_raw_buffer_load_b128(
+                           rx, lane_off, o + 16 * p4, 0));
+          tile[ks][2 * p4] = v2.x;
+          tile[ks][2 * p4 + 1] = v2.y;
+        }
+      } else {
+#pragma unroll
+        for (int p4 = 0; p4 < 2; ++p4) {
+          const float4 v4 = __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(
+                          rx, lane_off, o + 16 * p4, 0));
+          tile[ks][4 * p4] = v4.x;
+          tile[ks][4 * p4 + 1] = v4.y;
+          tile[ks][4 * p4 + 2] = v4.z;
+          tile[ks][4 * p4 + 3] = v4.w;
+        }
+      }
+    }
+    if (d != 16 * NKS) {  // wave-uniform
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          tile[ks][m] = 16 * ks + 8 * h + m < d ? tile[ks][m] : 0.0;
+    }
+  };
+
+  for (int64_t s0 = base + wv * 32; s0 < n; s0 += step) {
+    load_tile(s0);
+    float xx = 0.f;
+    bf16x8 xh[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int m = 0; m < 8; m += 2) {
+        const float x0 = (float)tile[ks][m];
+        const float x1 = (float)tile[ks][m + 1];
+        xx = fmaf(x0, x0, xx);
+        xx = fmaf(x1, x1, xx);
+        const bf16x2 h2 = __builtin_convertvector(f32x2{x0, x1}, bf16x2);
+        xh[ks][m] = h2[0];
+        xh[ks][m + 1] = h2[1];
+      }
+    {
+      float xa, xb;
+      pair_xor<32>(xx, xa, xb);
+      xx = xa + xb;
+    }
+    const int prv = pv;
+    const int64_t si = s0 + r;
+    float xn;
+    const float B2 = bound2_fast(bk, xx, xn);
+    const float B2t = bound2_fast(bkt, xx, xn);
+    const bool sane0 = (xn < 1e18f) & (xn * cm < 1e30f);
+    bool unique = false, two = false, many = false;
+    int i1 = 0, i2 = 0;
+    uint32_t mpk0 = 0, mpk1 = 0, mpk2 = 0;  // many: the candidate set
+    bool need3 = true;
+    if (hint) {
+      const bool pok = prv >= 0 && prv < k && si < n;
+      const uint64_t bad = __ballot(!pok && si < n);
+      if (__popcll(bad) <= 2 * B2_RTHR) {
+        const int p = pok ? prv : 0;
+        // ---- own block: columns = the tile's hinted centres p_c ----------
+        f32x16 dn;
+        {
+          bf16x8 of[NKS];
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks)
+            of[ks] = *(const bf16x8 *)(frag + ((int64_t)(p >> 5) * NKS + ks) *
+                                                  1024 +
+                                       ((p & 31) + 32 * h) * 16);
+          dn = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
+                      0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks)
+            dn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[ks], of[ks], dn, 0,
+                                                         0, 0);
+        }
+        // diagonal: row r sits in half (r >> 2) & 1, register
+        // (r & 3) + 4 (r >> 3); the other lane of the pair contributes 0
+        const int gsel = h == ((r >> 2) & 1) ? (r & 3) + 4 * (r >> 3) : -1;
+        float dg = 0.f;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) dg = gsel == g ? dn[g] : dg;
+        {
+          float da, db;
+          pair_xor<32>(dg, da, db);
+          dg = da + db;
+        }
+        const float ncp = ncn[p];
+        const float sp = dg - ncp;  // s_hat_p = |c_p|^2 + x.(-2 c_p)
+        const float T = pok ? sp + B2t : -INFINITY;
+        // ---- per-wave scratch: -T, hints, counts, own masks --------------
+        wave_sync();
+        if (h == 0) {
+          s_tn[r] = -T;
+          s_hp[r] = pok ? p : -1;
+          s_cnt[r] = 0;
+        }
+        for (int w = lane; w < 32 * nkw; w += 64) s_om[w] = 0u;
+        wave_sync();
+        uint32_t dup = 0;
+        if (h == 0 && pok) {
+          const uint32_t bit = 1u << ((p >> 5) & 31);
+          dup = atomicOr(&s_om[(p >> 10) * 32 + (p & 31)], bit) & bit;
+        }
+        {
+          int da, db;
+          pair_xor<32>((int)dup, da, db);
+          dup = (uint32_t)(da | db);
+        }
+        wave_sync();
+        f32x16 cin;
+        int pg[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 t4 = *(const f32x4 *)(s_tn + 8 * q + 4 * h);
+          const int4 p4 = *(const int4 *)(s_hp + 8 * q + 4 * h);
+          cin[4 * q] = t4.x;
+          cin[4 * q + 1] = t4.y;
+          cin[4 * q + 2] = t4.z;
+          cin[4 * q + 3] = t4.w;
+          pg[4 * q] = p4.x;
+          pg[4 * q + 1] = p4.y;
+          pg[4 * q + 2] = p4.z;
+          pg[4 * q + 3] = p4.w;
+        }
+        const uint32_t om0 = s_om[r];
+        auto push = [&](int row, float s, int j) {
+          const int slot = atomicAdd(&s_cnt[row], 1);
+          if (slot < B2_ENT)
+            s_ent[row * B2_ENT + slot] = make_int2(__float_as_int(s), j);
+        };
+        // own block: pairs (row, p) with p != p_row; the column of a centre
+        // hinted by several samples is tested once (dup)
+        {
+          float m = INFINITY;
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const float vg = pg[g] == p ? INFINITY : dn[g] + cin[g];
+            m = fminf(m, vg);
+          }
+          if (pok && !dup && m <= ncp) {
+#pragma unroll
+            for (int g = 0; g < 16; ++g)
+              if (pg[g] != p && dn[g] + cin[g] <= ncp)
+                push((g & 3) + 8 * (g >> 2) + 4 * h, dn[g] - ncp, p);
+          }
+        }
+        // ---- all centre blocks: lane = centre, registers = samples -------
+        auto rd = [&](int cb, bf16x8 (&f)[NKS], float &nc) {
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks)
+            f[ks] = *(const bf16x8 *)(frag + ((int64_t)cb * NKS + ks) * 1024 +
+                                      lane * 16);
+          nc = ncn[cb * 32 + r];
+        };
+        auto mm = [&](const bf16x8 (&f)[NKS], f32x16 &acc) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[0], f[0], cin, 0, 0,
+                                                        0);
+#pragma unroll
+          for (int ks = 1; ks < NKS; ++ks)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[ks], f[ks], acc, 0,
+                                                          0, 0);
+        };
+        // whole-block test: the 16 rows' min against -|c_j|^2, or against a
+        // NaN (never passes) where centre j is a hinted one (own block)
+        auto test = [&](int cb, const f32x16 &acc, float nc, float &thr,
+                        bool &any) {
+          const uint32_t w = W1 ? om0 : s_om[(cb >> 5) * 32 + r];
+          const int own = (int)(w << (31 - (cb & 31))) >> 31;
+          thr = __uint_as_float(((uint32_t)own & 0xff800000u) |
+                                __float_as_uint(nc));
+          float mp[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            mp[i] = __builtin_amdgcn_fmed3f(acc[2 * i], acc[2 * i + 1], ninf);
+          const float a = fminf(fminf(mp[0], mp[1]), mp[2]);
+          const float b = fminf(fminf(mp[3], mp[4]), mp[5]);
+          const float c = fminf(fminf(mp[6], mp[7]), a);
+          any = fminf(b, c) <= thr;
+        };
+        auto append = [&](int cb, const f32x16 &acc, float thr, float nc,
+                          bool any) {
+          if (any) {
+            const int j = cb * 32 + r;
+#pragma unroll
+            for (int g = 0; g < 16; ++g)
+              if (acc[g] <= thr)
+                push((g & 3) + 8 * (g >> 2) + 4 * h, (acc[g] - cin[g]) - nc, j);
+          }
+        };
+        {
+          f32x16 acc_a, acc_b;
+          bf16x8 fa[NKS], fb[NKS];
+          float na, nb, ta, tb;
+          bool ga, gb;
+          auto interleave = [&]() {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1 + NKS, 0);  // DS rd
+#pragma unroll
+            for (int i = 0; i < NKS; ++i) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+              __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
+            }
+          };
+          rd(0, fa, na);
+          mm(fa, acc_a);
+          int cb = 0;
+          for (; cb + 2 < nkb; cb += 2) {
+            rd(cb + 1, fb, nb);
+            test(cb, acc_a, na, ta, ga);
+            mm(fb, acc_b);
+            interleave();
+            append(cb, acc_a, ta, na, ga);
+            rd(cb + 2, fa, na);
+            test(cb + 1, acc_b, nb, tb, gb);
+            mm(fa, acc_a);
+            interleave();
+            append(cb + 1, acc_b, tb, nb, gb);
+          }
+          if (cb + 1 < nkb) {
+            rd(cb + 1, fb, nb);
+            test(cb, acc_a, na, ta, ga);
+            mm(fb, acc_b);
+            interleave();
+            append(cb, acc_a, ta, na, ga);
+            test(cb + 1, acc_b, nb, tb, gb);
+            append(cb + 1, acc_b, tb, nb, gb);
+          } else {
+            test(cb, acc_a, na, ta, ga);
+            append(cb, acc_a, ta, na, ga);
+          }
+        }
+        // ---- decision over the hint and the kept entries ------------------
+        wave_sync();
+        const int cnt = s_cnt[r];
+        float sv[B2_ENT + 1];
+        int cv[B2_ENT + 1];
+        bool ok[B2_ENT + 1];
+        sv[0] = sp;
+        cv[0] = p;
+        ok[0] = true;
+#pragma unroll
+        for (int e = 0; e < B2_ENT; ++e) {
+          const int2 en = s_ent[r * B2_ENT + e];
+          sv[e + 1] = __int_as_float(en.x);
+          cv[e + 1] = en.y;
+          ok[e + 1] = e < cnt;
+        }
+        const bool over = cnt > B2_ENT || !pok || !sane0 || !(T < 1e30f);
+        float bs = INFINITY;
+        int bc = 0x7fffffff;
+#pragma unroll
+        for (int e = 0; e <= B2_ENT; ++e)
+          if (ok[e] && (sv[e] < bs || (sv[e] == bs && cv[e] < bc))) {
+            bs = sv[e];
+            bc = cv[e];
+          }
+        int namb = 0, other = 0;
+        uint32_t pk[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};
+#pragma unroll
+        for (int e = 0; e <= B2_ENT; ++e)
+          if (ok[e] && !(sv[e] - bs > B2t)) {
+#pragma unroll
+            for (int w = 0; w < 6; ++w)
+              if (w == namb)
+                pk[w >> 1] = (w & 1) ? (pk[w >> 1] & 0xffffu) |
+                                           ((uint32_t)cv[e] << 16)
+                                     : (pk[w >> 1] & 0xffff0000u) |
+                                           (uint32_t)cv[e];
+            ++namb;
+            other = cv[e] != bc ? cv[e] : other;
+          }
+        const uint64_t mo = __ballot(over && si < n && h == 0);
+        ++t_tiles;
+        if (__popcll(mo) <= B2_RTHR) {
+          ++t_done;
+          need3 = false;
+          unique = !over && namb == 1;
+          two = !over && namb == 2;
+          many = !over && namb >= 3;
+          i1 = bc;
+          i2 = other;
+          mpk0 = pk[0];
+          mpk1 = pk[1];
+          mpk2 = pk[2];
+        }
+      }
+    }
+    if (need3) {
+      // ---- top-3 pass (no usable hint): b1's layout, centres on the rows --
+      auto chain = [&](int cb, f32x16 &accv) {
+        const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
+        const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
+        accv = f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                      c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const bf16x8 ah =
+              *(const bf16x8 *)(frag + ((int64_t)cb * NKS + ks) * 1024 +
+                                lane * 16);
+          accv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xh[ks], accv, 0,
+                                                         0, 0);
+        }
+      };
+      float r1 = INFINITY, r2 = INFINITY, r3 = INFINITY;
+      int ii1 = 0, ii2 = 0, ii3 = 0;
+      for (int g0 = 0; g0 < nkb; g0 += GB) {
+        const int g1 = min(nkb, g0 + GB);
+        float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
+        float e1 = INFINITY, e2 = INFINITY, e3 = INFINITY;
+        auto score = [&](int cb, const f32x16 &accv) {
+          const uint32_t t0 = opaque_s32((uint32_t)((cb - g0) * 16));
+#pragma unroll
+          for (int g = 0; g < 16; g += 2) {
+            const float sa =
+                __uint_as_float((__float_as_uint(accv[g]) & vmask) | (t0 + g));
+            const float sb = __uint_as_float(
+                (__float_as_uint(accv[g + 1]) & vmask) | (t0 + g + 1));
+            b3 = __builtin_amdgcn_fmed3f(b2, b3, sa);
+            b2 = __builtin_amdgcn_fmed3f(b1, b2, sa);
+            b1 = min_nc(b1, sa, ninf);
+            e3 = __builtin_amdgcn_fmed3f(e2, e3, sb);
+            e2 = __builtin_amdgcn_fmed3f(e1, e2, sb);
+            e1 = min_nc(e1, sb, ninf);
+          }
+        };
+        f32x16 acc_a, acc_b;
+        chain(g0, acc_a);
+        int cb = g0;
+        for (; cb + 2 <= g1; cb += 2) {
+          chain(cb + 1, acc_b);
+          score(cb, acc_a);
+          if (cb + 2 < g1) chain(cb + 2, acc_a);
+          score(cb + 1, acc_b);
+        }
+        if (cb < g1) score(cb, acc_a);
+        auto gidx = [&](float q) {
+          const uint32_t tg = __float_as_uint(q) & PACK2_MASK;
+          const int g = (int)(tg & 15);
+          return (g0 + (int)(tg >> 4)) * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+        };
+        auto ins = [&](float q) {
+          const int qi = gidx(q);
+          const bool c1 = q < r1, c2 = q < r2, c3 = q < r3;
+          r3 = c2 ? r2 : (c3 ? q : r3);
+          ii3 = c2 ? ii2 : (c3 ? qi : ii3);
+          r2 = c1 ? r1 : (c2 ? q : r2);
+          ii2 = c1 ? ii1 : (c2 ? qi : ii2);
+          r1 = c1 ? q : r1;
+          ii1 = c1 ? qi : ii1;
+        };
+        ins(b1);
+        ins(b2);
+        ins(b3);
+        ins(e1);
+        ins(e2);
+        ins(e3);
+      }
+      {  // merge the sample's two lanes (same triple on both)
+        const float o1 = __shfl_xor(r1, 32, 64), o2 = __shfl_xor(r2, 32, 64),
+                    o3 = __shfl_xor(r3, 32, 64);
+        const int j1 = __shfl_xor(ii1, 32, 64), j2 = __shfl_xor(ii2, 32, 64),
+                  j3 = __shfl_xor(ii3, 32, 64);
+        auto lt = [](float a, int ia, float b, int ib) {
+          return a < b || (a == b && ia < ib);
+        };
+        auto ins3 = [&](float q, int qi) {
+          const bool c1 = lt(q, qi, r1, ii1), c2 = lt(q, qi, r2, ii2),
+                     c3 = lt(q, qi, r3, ii3);
+          r3 = c2 ? r2 : (c3 ? q : r3);
+          ii3 = c2 ? ii2 : (c3 ? qi : ii3);
+          r2 = c1 ? r1 : (c2 ? q : r2);
+          ii2 = c1 ? ii1 : (c2 ? qi : ii2);
+          r1 = c1 ? q : r1;
+          ii1 = c1 ? qi : ii1;
+        };
+        ins3(o1, j1);
+        ins3(o2, j2);
+        ins3(o3, j3);
+      }
+      const bool sane = sane0 & (r1 < 1e30f);
+      unique = sane & (r2 - r1 > B2);
+      two = sane & !unique & (r3 - r1 > B2);
+      i1 = ii1;
+      i2 = ii2;
+    }
+    const bool valid = si < n && h == 0;
+    const int prev = delta ? prv : -1;
+    // 3..6 candidates of the threshold pass -> the N-candidate list
+    bool nlisted = false;
+    {
+      const uint64_t mn = __ballot(valid && many);
+      const int addn = __popcll(mn);
+      if (addn && listing && nl_cnt + addn <= B1_NCAP) {
+        if (valid && many)
+          nl[nl_cnt + lane_prefix(mn)] =
+              make_int4((int)(si - base), (int)mpk0, (int)mpk1, (int)mpk2);
+        nl_cnt += addn;
+        nlisted = many;
+      }
+    }
+    // two candidates -> candidate list, more -> re-check list
+    const uint64_t mc = __ballot(valid && two);
+    const uint64_t mt = __ballot(valid && !unique && !two && !nlisted);
+    const int addc = __popcll(mc), addt = __popcll(mt);
+    if (listing && cl_cnt + addc <= B1_CAP) {
+      if (valid && two)
+        cl[cl_cnt + lane_prefix(mc)] =
+            make_int2((int)(si - base), i1 | (i2 << 16));
+      cl_cnt += addc;
+    } else {
+      tl_over += addc;
+    }
+    if (listing && tl_cnt + addt <= TL_CAP) {
+      if (valid && !unique && !two && !nlisted)
+        wl[tl_cnt + lane_prefix(mt)] = make_int2((int)(si - base), prev);
+      tl_cnt += addt;
+    } else {
+      tl_over += addt;
+    }
+    // a label equal to the incoming one (the hint) needs no store; an
+    // N-listed sample keeps it until k_candn writes the winner.  A sample
+    // that overflowed a list keeps -(prev + 2): the label scan finds it.
+    if (valid && !nlisted && !(unique && i1 == (hint ? prv : prev)))
+      lab_out[si] = unique ? i1 : -(prev + 2);
+  }
+  if (lane == 0 && listing) {
+    v.tcount[wv] = tl_cnt;
+    v.ccount[wv] = cl_cnt;
+    v.ncount[wv] = nl_cnt;
+  }
+  if (lane == 0 && t_tiles) {  // diagnostics (dkm_screen_counters)
+    atomicAdd((unsigned long long *)&v.hdr->reserved[0],
+              (unsigned long long)t_tiles);
+    atomicAdd((unsigned long long *)&v.hdr->reserved[1],
+              (unsigned long long)t_done);
+  }
+  if (lane == 0 && tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
+}
+
+size_t b2_lds_bytes(int64_t k, int64_t d) {
+  const int64_t nkb = kpad32(k) / 32, nkw = (nkb + 31) / 32;
+  return (size_t)nkb * (dpad16(d) / 16) * 1024 + (size_t)nkb * 256 +
+         (size_t)(SB2 / 64) * (B2_SCR_FIXED + 128 * nkw);
+}
+
+// DKM_B1_LEGACY=1 runs k_screen_b1 instead (A/B and its parity tests); read
+// per launch so that one process can run both
+bool b2_enabled() {
+  const char *e = getenv("DKM_B1_LEGACY");
+  return !(e && *e && *e != '0');
+}
+
+template <class TX>
+int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
+                     const WsView &v, int32_t *lab_out, int64_t base, int hint,
+                     int cus, hipStream_t s, int *nseg) {
+  const size_t lds = b2_lds_bytes(k, d);
+  if (lds > 160 * 1024) return 1;  // caller uses k_screen_b1
+  const int nks = (int)(dpad16(d) / 16);
+  const bool w1 = kpad32(k) <= 1024;
+  const void *kf = nullptr;
+  switch (nks) {
+#define DKM_B2(N)                                                  \
+  case N:                                                          \
+    kf = w1 ? (const void *)k_screen_b2<TX, N, true>               \
+            : (const void *)k_screen_b2<TX, N, false>;             \
+    break;
+    DKM_B2(1) DKM_B2(2) DKM_B2(3) DKM_B2(4)
+    DKM_B2(5) DKM_B2(6) DKM_B2(7) DKM_B2(8)
+#undef DKM_B2
+    default:
+      return fail(DKM_E_ARG, "screen_b2: d too large");
+  }
+  if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "screen_b2: LDS attribute");
+  const int64_t need = (end - base + 32 * (SB2 / 64) - 1) / (32 * (SB2 / 64));
+  const unsigned g =
+      (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)cus));
+  *nseg = (int)std::min<int64_t>((int64_t)g * (SB2 / 64),
+                                 std::min(TL_SEGS, B1_SEGS));
+  const int delta = 0;  // labels only (the sums come from the labels)
+  switch (nks) {
+#define DKM_B2L(N)                                                      \
+  case N:                                                               \
+    if (w1)                                                             \
+      k_screen_b2<TX, N, true><<<g, SB2, lds, s>>>(                     \
+          X, end, d, ldx, k, v, lab_out, base, delta, hint);            \
+    else                                                                \
+      k_screen_b2<TX, N, false><<<g, SB2, lds, s>>>(                    \
+          X, end, d, ldx, k, v, lab_out, base, delta, hint);            \
+    break;
+    DKM_B2L(1) DKM_B2L(2) DKM_B2L(3) DKM_B2L(4)
+    DKM_B2L(5) DKM_B2L(6) DKM_B2L(7) DKM_B2L(8)
+#undef DKM_B2L
+  }
+  return check_launch("screen assignment (single product, centres on lanes)");
+}
+
+template int launch_screen_b2<double>(const double *, int64_t, int, int64_t,
+                                      int, const WsView &, int32_t *, int64_t,
+                                      int, int, hipStream_t, int *);
+template int launch_screen_b2<float>(const float *, int64_t, int, int64_t, int,
+                                     const WsView &, int32_t *, int64_t, int,
+                                     int, hipStream_t, int *);
+
+}  // namespace dkm

@@ -42,6 +42,8 @@ struct Rccl {
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclCommDestroy) destroy = nullptr;
   decltype(&ncclGetErrorString) err = nullptr;
+  decltype(&ncclCommCount) count = nullptr;
+  decltype(&ncclCommUserRank) user_rank = nullptr;
 };
 
 std::mutex g_mu;
@@ -66,8 +68,10 @@ int load_rccl() {
   r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
   r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
   r.err = (decltype(r.err))dlsym(h, "ncclGetErrorString");
+  r.count = (decltype(r.count))dlsym(h, "ncclCommCount");
+  r.user_rank = (decltype(r.user_rank))dlsym(h, "ncclCommUserRank");
   if (!r.get_id || !r.init_rank || !r.init_all || !r.all_reduce ||
-      !r.destroy || !r.err)
+      !r.destroy || !r.err || !r.count || !r.user_rank)
     return dkm::fail(DKM_E_COMM, "librccl lacks an nccl entry point");
   g_r = r;
   return 0;
@@ -172,6 +176,34 @@ int dkm_allreduce_finalize(void) {
   }
   g_comms.clear();
   return r;
+}
+
+int dkm_allreduce_finalize_device(int device) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_comms.find(device);
+  if (it == g_comms.end()) return 0;
+  const ncclResult_t rc = g_r.destroy(it->second);
+  g_comms.erase(it);
+  return rc ? rccl_fail("ncclCommDestroy", rc) : 0;
+}
+
+int dkm_allreduce_available(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return load_rccl();
+}
+
+int dkm_allreduce_comm_info(int device, int *nranks, int *rank) {
+  if (!nranks || !rank) return dkm::fail(DKM_E_ARG, "allreduce_comm_info: NULL");
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_comms.find(device);
+  if (it == g_comms.end())
+    return dkm::fail(DKM_E_ARG, "allreduce_comm_info: no communicator on "
+                                "device " + std::to_string(device));
+  if (ncclResult_t rc = g_r.count(it->second, nranks))
+    return rccl_fail("ncclCommCount", rc);
+  if (ncclResult_t rc = g_r.user_rank(it->second, rank))
+    return rccl_fail("ncclCommUserRank", rc);
+  return 0;
 }
 
 }  // extern "C"

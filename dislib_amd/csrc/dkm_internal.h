@@ -139,6 +139,16 @@ struct WsView {
   int32_t *smoved; // samples whose label changed (delta sums)
 };
 
+// Single-product screen with the centres on the lanes (dkm_b2.hip): the
+// threshold pass without per-block norm reads.  Returns 1 (nothing
+// launched) when its LDS image does not fit; the caller runs k_screen_b1.
+bool b2_enabled();
+size_t b2_lds_bytes(int64_t k, int64_t d);
+template <class TX>
+int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
+                     const WsView &v, int32_t *lab_out, int64_t base,
+                     int hint, int cus, hipStream_t s, int *nseg);
+
 // Sorted sums: counting sort of the sample indices by label (LDS histograms
 // of k bins: k <= SORT_KMAX), then segmented row sums.
 constexpr int SORT_KMAX = 16384;

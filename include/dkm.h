@@ -182,6 +182,15 @@ int dkm_allreduce_sum_f64(double *buf, int64_t count, int device,
                           void *stream);
 /* Destroy every communicator of this process. */
 int dkm_allreduce_finalize(void);
+/* Destroy the communicator of `device` only (0 when it has none). */
+int dkm_allreduce_finalize_device(int device);
+/* 0 when librccl loads and has every entry point used here: a cheap,
+ * non-blocking check every rank makes before the collective
+ * ncclCommInitRank, so that the ranks agree on a fallback up front. */
+int dkm_allreduce_available(void);
+/* The communicator of `device`: its rank count (ncclCommCount) and this
+ * rank's index in it (ncclCommUserRank).  DKM_E_ARG if it has none. */
+int dkm_allreduce_comm_info(int device, int *nranks, int *rank);
 
 /* Synthetic make_blobs rows [row0, row0+n) into X (n x d, ld = d), blob ids
  * into blob (nullable).  Counter-based: any row range regenerates
@@ -193,6 +202,14 @@ int dkm_make_blobs_f64(double *X, int64_t row0, int64_t n, int64_t d,
 /* Diagnostics of the last SCREEN32 call on this workspace (device -> host,
  * synchronous on `stream`): number of samples sent to the exact re-check.  */
 int dkm_screen_stats(const void *ws, int64_t *n_rechecked, void *stream);
+
+/* Build flags of this library: 0 for a product build.  Non-zero
+ * (DKM_BUILD_TIMING_ONLY) when it was compiled with an A/B timing probe
+ * that invalidates results (DKM_AB_B1_PROBE, DKM_DBG_NOCOMPUTE, ...): such a
+ * library refuses every assignment call.  tests/test_isa_guard.py checks
+ * that the in-tree library reports 0. */
+#define DKM_BUILD_TIMING_ONLY 1
+int dkm_build_flags(void);
 
 /* ------------------------------------------------------------------------
  * Distance-primitive reuse outside the Lloyd loop (SURVEY.md section 8

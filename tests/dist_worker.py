@@ -27,12 +27,25 @@ CASES = {
     "gemm": (6000, 200, 20, 40, 500, 4, 0.0, 3, 2),
     "none": (9000, 8, 6, 6, 1000, 8, 1e-6, None, 8),
     "ragged": (7001, 24, 9, 9, 700, 5, 0.0, 5, 8),
+    # k x d sums beyond LDS: the single-product screen with label hints
+    # (k_screen_b2) on both ranks, delta sums, refresh every 3
+    "b2": (24000, 64, 200, 200, 2000, 6, 0.0, 0, 3),
+    # CSR Subsets (the sparse screen + exact resolve), 10 entries per row
+    "csr": (2000, 300, 0, 8, 250, 4, 0.0, 2, 2),
 }
 
 
 def data(case):
     from sklearn.datasets import make_blobs
     n, d, blobs = CASES[case][:3]
+    if case == "csr":
+        import scipy.sparse as sp
+        rng = np.random.default_rng(11)
+        cols = np.sort(np.stack([rng.choice(d, 10, replace=False)
+                                 for _ in range(n)]), axis=1)
+        indptr = np.arange(0, 10 * n + 1, 10)
+        return sp.csr_matrix((rng.random(10 * n), cols.reshape(-1),
+                              indptr), shape=(n, d))
     x, _ = make_blobs(n_samples=n, n_features=d, centers=blobs,
                       center_box=(-8, 8), random_state=42)
     return x
@@ -66,7 +79,9 @@ def main():
     ds = shard_dataset(load_data(x, sub))
     km = KMeans(n_clusters=k, max_iter=iters, tol=tol, random_state=rs)
     km.fit_predict(ds)
-    np.savez("%s.%d.npz" % (a.out, rank), centers=km.centers,
+    cen = km.centers.toarray() if hasattr(km.centers, "toarray") else \
+        km.centers
+    np.savez("%s.%d.npz" % (a.out, rank), centers=cen,
              n_iter=km.n_iter, labels=ds.labels_int32(), init=init["c"],
              refresh=np.array(km_mod.REFRESH))
     dist.barrier()

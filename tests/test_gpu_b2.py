@@ -1,0 +1,166 @@
+"""GPU parity of the label-hinted threshold pass of the single-product
+screen: k_screen_b2 (centres on the lanes, dkm_b2.hip) and the k_screen_b1
+it replaces (DKM_B1_LEGACY=1), against the oracle's restatement of the
+reference assignment (dislib cluster/kmeans/base.py:171-173, 204-205).
+
+Shapes cover every K-step count the kernels instantiate that the LDS admits,
+k % 32 != 0 (hints pointing into a partial last block), an odd number of
+centre blocks (the pipeline's tail), k > 1024 (own masks of several words),
+and a shape whose b2 image does not fit LDS (the b1 fallback).  Hint kinds:
+the right labels, 30 % wrong, and exact duplicate centres placed in EVERY
+centre block with the hint on the later copy -- every block position then
+takes the append branch, and the first index must win the exact tie.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import kmeans_oracle as orc
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.fixture(params=["b2", "b1"])
+def variant(request):
+    old = os.environ.get("DKM_B1_LEGACY")
+    os.environ["DKM_B1_LEGACY"] = "1" if request.param == "b1" else "0"
+    yield request.param
+    if old is None:
+        os.environ.pop("DKM_B1_LEGACY", None)
+    else:
+        os.environ["DKM_B1_LEGACY"] = old
+
+
+def _hinted(x, C, hint, acc_kind="partial"):
+    from dislib_amd import _device, _lib
+    from dislib_amd.data import load_data
+    dev = torch.device("cuda", 0)
+    ds = load_data(x, subset_size=x.shape[0])
+    dd = ds._device_data()
+    k, d = C.shape
+    Ct = torch.from_numpy(np.ascontiguousarray(C)).to(dev)
+    ws = _device.Workspace(k, d, dd.n, dev)
+    acc = torch.zeros(k * (d + 1), dtype=torch.float64, device=dev)
+    lab = torch.from_numpy(np.asarray(hint).astype(np.int32)).to(dev)
+    _device.prepare(Ct, ws, acc)
+    if acc_kind == "partial":
+        _device.partial_sum(dd, Ct, ws, lab, acc, _lib.MODE_BF16)
+    else:
+        _device.assign_delta(dd, Ct, ws, lab, acc, _lib.MODE_BF16)
+    a = acc.cpu().numpy()
+    return lab.cpu().numpy(), a[:k * d].reshape(k, d), a[k * d:]
+
+
+def _problem(n, d, k, seed):
+    rng = np.random.default_rng(seed)
+    blobs = rng.uniform(-10, 10, (k, d))
+    x = blobs[rng.integers(0, k, n)] + rng.standard_normal((n, d))
+    C = blobs + rng.standard_normal((k, d)) * 0.3
+    return rng, x, C
+
+
+def _dups_every_block(rng, C):
+    """An exact copy of some centre in every 32-centre block (a different
+    slot per block); returns (copy, original) index pairs."""
+    k = C.shape[0]
+    nkb = (k + 31) // 32
+    pairs = []
+    used = set()
+    for b in range(nkb):
+        j = min(32 * b + (5 * b + 3) % 32, k - 1)
+        p = (j + 37 + 11 * b) % k
+        if j in used or p in used or j == p:
+            continue
+        used.update((j, p))
+        C[j] = C[p]
+        pairs.append((j, p))
+    return pairs
+
+
+@pytest.mark.parametrize("d,k", [(16, 300), (32, 600), (64, 1000), (64, 990),
+                                 (48, 777), (96, 500), (16, 2000),
+                                 (128, 560)])
+@pytest.mark.parametrize("kind", ["exact", "noisy", "dups"])
+def test_threshold_pass_shapes(variant, d, k, kind):
+    n = 30000
+    rng, x, C = _problem(n, d, k, 1000 * d + k)
+    if kind == "dups":
+        pairs = _dups_every_block(rng, C)
+        # samples at both copies of each pair: an exact tie between them
+        m = len(pairs)
+        idx = rng.integers(0, n, 40 * m)
+        for t, i in enumerate(idx):
+            j, p = pairs[t % m]
+            x[i] = C[p] + rng.standard_normal(d)
+    rl, rs, rc = orc.partial_sum(x, C)
+    if kind == "exact":
+        hint = rl
+    elif kind == "noisy":
+        hint = np.where(rng.random(n) < 0.3, rng.integers(0, k, n), rl)
+    else:
+        # hint = the LATER copy of a duplicated pair (the reference picks the
+        # first index: the pass must find the earlier copy as a tie)
+        _, inv = np.unique(C, axis=0, return_inverse=True)
+        inv = np.asarray(inv).reshape(-1)
+        last = {}
+        for c in range(k):
+            last[inv[c]] = c
+        hint = np.array([last[inv[c]] for c in rl])
+        assert (hint != rl).sum() > 0
+    lab, sums, cnt = _hinted(x, C, hint)
+    assert np.array_equal(lab, rl), (lab != rl).sum()
+    assert np.array_equal(cnt, rc.astype(np.float64))
+    err = np.max(np.abs(sums - rs) / np.maximum(np.abs(rs), 1.0))
+    assert err <= 1e-12
+
+
+@pytest.mark.parametrize("d,k", [(64, 1000), (16, 2000)])
+def test_threshold_pass_delta(variant, d, k):
+    """dkm_assign_delta with previous labels as the hint (the fit loop's
+    call): labels exact and the delta of the sums."""
+    n = 30000
+    rng, x, C = _problem(n, d, k, 7 * d + k)
+    prev = orc.predict_labels(x, C + 0.2 * rng.standard_normal(C.shape))
+    prev[rng.random(n) < 0.01] = -1
+    rl, rs, rc = orc.partial_sum(x, C)
+    lab, sums, cnt = _hinted(x, C, prev, acc_kind="delta")
+    assert np.array_equal(lab, rl)
+    ps = np.zeros((k, d))
+    pc = np.zeros(k)
+    ok = prev >= 0
+    np.add.at(ps, prev[ok], x[ok])
+    np.add.at(pc, prev[ok], 1)
+    assert np.array_equal(cnt, rc - pc)
+    err = np.max(np.abs(sums - (rs - ps)) / np.maximum(np.abs(rs), 1.0))
+    assert err <= 1e-11
+
+
+def test_threshold_pass_tail_and_hint_edge_cases(variant):
+    """n not a multiple of 32 (a partial last tile), hints at -1, k, k-1
+    (the last, partially filled block) and 0, a constant hint for a whole
+    wave tile, and a crowded group (overfull kept lists: top-3 fallback)."""
+    n, d, k = 20011, 64, 1000
+    rng, x, C = _problem(n, d, k, 5)
+    z = rng.uniform(-10, 10, d)
+    C[960:] = z + 0.05 * rng.standard_normal((40, d))
+    near = rng.random(n) < 0.05
+    x[near] = z + rng.standard_normal((int(near.sum()), d))
+    rl, rs, rc = orc.partial_sum(x, C)
+    hint = rl.copy()
+    sel = rng.random(n)
+    hint[sel < 0.02] = -1
+    hint[(sel >= 0.02) & (sel < 0.04)] = k
+    hint[(sel >= 0.04) & (sel < 0.06)] = k - 1
+    hint[(sel >= 0.06) & (sel < 0.08)] = 0
+    hint[64:96] = 17
+    lab, sums, cnt = _hinted(x, C, hint)
+    assert np.array_equal(lab, rl)
+    assert np.array_equal(cnt, rc.astype(np.float64))

@@ -85,7 +85,8 @@ def _run_world2(case, tmp_path):
     return [dict(np.load("%s.%d.npz" % (out, i))) for i in range(2)]
 
 
-@pytest.mark.parametrize("case", ["dense", "gemm", "none", "ragged"])
+@pytest.mark.parametrize("case", ["dense", "gemm", "none", "ragged", "b2",
+                                  "csr"])
 def test_world2_fit_predict_vs_oracle(case, tmp_path):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import dist_worker as w
@@ -104,12 +105,13 @@ def test_world2_fit_predict_vs_oracle(case, tmp_path):
     real_init = orc.init_centers
     orc.init_centers = lambda *a: r0["init"].copy()
     try:
-        rl = ref.fit(blocks, set_labels=True)
+        rl = ref.fit(blocks, sparse=case == "csr", set_labels=True)
     finally:
         orc.init_centers = real_init
     assert int(r0["n_iter"]) == ref.n_iter
     lab = np.concatenate([r0["labels"], r1["labels"]])
     assert np.array_equal(lab, rl)
-    err = np.max(np.abs(r0["centers"] - ref.centers) /
-                 np.maximum(np.abs(ref.centers), 1.0))
+    rc = ref.centers.toarray() if hasattr(ref.centers, "toarray") else \
+        ref.centers
+    err = np.max(np.abs(r0["centers"] - rc) / np.maximum(np.abs(rc), 1.0))
     assert err <= 1e-9, err

@@ -27,7 +27,7 @@ def _flags():
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not present")
 @pytest.mark.parametrize("src", ["dkm_dense.hip", "dkm_util.hip",
-                                 "dkm_sparse.hip"])
+                                 "dkm_sparse.hip", "dkm_b2.hip"])
 def test_no_packed_fp32_valu(src, tmp_path):
     out = tmp_path / (src + ".s")
     cmd = [HIPCC] + _flags() + ["-S", "--cuda-device-only",
@@ -38,3 +38,16 @@ def test_no_packed_fp32_valu(src, tmp_path):
     bad = sorted(set(re.findall(r"\bv_pk_\w*f32\b", asm)))
     assert not bad, "packed fp32 VALU in %s: %s" % (src, bad)
     assert "-fno-slp-vectorize" in _flags()
+
+
+def test_product_build_has_no_timing_probe():
+    """The in-tree libdkm.so was built without any result-invalidating A/B
+    probe (DKM_AB_B1_PROBE, DKM_DBG_NOCOMPUTE, DKM_DBG_NOLOAD): those exist
+    for timing-only variant libraries (csrc/variants.sh)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from dislib_amd import _lib
+    assert _lib.load().dkm_build_flags() == 0
+    src = open(os.path.join(CSRC, "Makefile")).read()
+    for m in ("DKM_AB_B1_PROBE", "DKM_DBG_NOCOMPUTE", "DKM_DBG_NOLOAD"):
+        assert m not in src

@@ -1,0 +1,19 @@
+#!/bin/bash
+# SQ-only counter passes (rocprofv3 --pmc, kernel-trace only) of bench.py at
+# PMC_N rows.  usage: BENCH_ARGS=... bash tools/pmc_session_sq.sh TAG
+TAG=${1:-r03}; OUT=gpurun_out/${TAG}_pmc; mkdir -p $OUT; export TMPDIR=/tmp
+N=${PMC_N:-20000000}
+PROG=(python bench.py --n $N --steps 8 --warmup 4 --no-cpu --only-headline $BENCH_ARGS)
+run() {  # name counters...
+  local name=$1; shift
+  echo "== pmc $name: $*"
+  timeout -k 10 240 rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
+     -d $OUT/$name -o run -- "${PROG[@]}" > $OUT/$name.log 2>&1
+  local rc=$?; echo "== rc=$rc"; tail -2 $OUT/$name.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo STOP; exit $rc; fi
+}
+run p1 SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE
+run p2 SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT
+run p4 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_VALU_MFMA_BUSY_CYCLES
+python tools/pmc_summary.py $OUT --n $N > $OUT/summary.txt 2>&1
+echo "== done"
