@@ -228,7 +228,7 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
         st.partial()                  # the dominant kernel(s), same stream
         ev[i][1].record()
         st.reduce_update()
-        st.flag.item()                # the per-iteration convergence read
+        st.read_flags()               # the per-iteration convergence read
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

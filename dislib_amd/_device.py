@@ -213,10 +213,16 @@ def assign_delta(dd, C, ws, labels, delta, mode):
                "dkm_assign_delta")
 
 
-def add_(y, x):
+def add_(y, x, nonzero=None):
+    """y += x; with ``nonzero`` (a device int32 element view): 1 there if any
+    x != 0, else 0."""
     so = _lib.lib()
-    _lib.check(so.dkm_add_f64(ptr(y), ptr(x), y.numel(), stream_ptr()),
-               "dkm_add_f64")
+    if nonzero is None:
+        _lib.check(so.dkm_add_f64(ptr(y), ptr(x), y.numel(), stream_ptr()),
+                   "dkm_add_f64")
+    else:
+        _lib.check(so.dkm_add_f64_nz(ptr(y), ptr(x), y.numel(), ptr(nonzero),
+                                     stream_ptr()), "dkm_add_f64_nz")
 
 
 def predict(dd, C, ws, labels, mode):

@@ -144,6 +144,10 @@ class KMeans:
 # add rounding of at most REFRESH * 2^-52 * (|S_old| + |moved rows|) per
 # sum element (a shrinking cluster keeps the error of its larger past
 # sums); the fit tests pin the centres at 1e-9 of the oracle with 8.
+# A refresh is skipped when no delta since the last one held a nonzero:
+# then no sample changed cluster, the running sums are bit-identical to
+# that last full recomputation, and they ARE the sums of the current
+# assignment (a converged fit stops re-reading X for them).
 REFRESH = int(os.environ.get("DKM_REFRESH", "8"))
 
 
@@ -180,7 +184,11 @@ class _Lloyd:
         self.acc = t.empty(k * (d + 1), dtype=t.float64, device=dd.device)
         self.state = t.zeros(k * (d + 1), dtype=t.float64, device=dd.device)
         self.diff = t.zeros(k + 1, dtype=t.float64, device=dd.device)
-        self.flag = t.zeros(1, dtype=t.int32, device=dd.device)
+        # [converged, delta nonzero]: read together once per iteration
+        self.flag = t.zeros(2, dtype=t.int32, device=dd.device)
+        self.dirty = False     # a delta since the last full recomputation
+                               # moved a sample
+        self._was_full = True
         self.labels = t.full((max(dd.n, 1),), -1, dtype=t.int32,
                              device=dd.device)
         self.set_labels = set_labels
@@ -206,7 +214,7 @@ class _Lloyd:
             prepare(self.C, self.ws, self.acc, csr=self.sparse)
 
     def _full(self):
-        return self.it % self.refresh == 0
+        return self.it == 0 or (self.it % self.refresh == 0 and self.dirty)
 
     def partial(self):
         """The hot kernel: fused assignment over all resident samples, full
@@ -237,18 +245,32 @@ class _Lloyd:
         from .._device import add_, update
         with self._on():
             _shard.allreduce_sum_(self.acc)
-            if self._full():
+            self._was_full = self._full()
+            if self._was_full:
                 self.state.copy_(self.acc)
             else:
-                add_(self.state, self.acc)
+                # every rank adds the same all-reduced delta: the ranks'
+                # nonzero flags, and so their refresh decisions, agree
+                add_(self.state, self.acc, self.flag[1:])
             update(self.state, self.C, self.sums_mode, self.tol, self.diff,
-                   self.flag)
+                   self.flag[:1])
         self.it += 1
+
+    def read_flags(self):
+        """The iteration's one device->host read (the reference's
+        per-iteration sync, base.py:143): converged?, and whether the delta
+        moved a sample (the refresh bookkeeping)."""
+        conv, nz = self.flag.tolist()
+        if self._was_full:
+            self.dirty = False
+        elif nz:
+            self.dirty = True
+        return bool(conv)
 
     def step(self):
         self.assign()
         self.reduce_update()
-        return bool(self.flag.item())
+        return self.read_flags()
 
     def criterion(self):
         return float(self.diff[0].item())

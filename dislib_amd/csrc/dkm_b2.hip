@@ -50,13 +50,34 @@ namespace dkm {
 #ifndef DKM_AB_SB2
 #define DKM_AB_SB2 768
 #endif
+// A/B timing probes (results invalid; dkm_build_flags reports them):
+// 1 = no centre-block loop, 2 = the loop's chains and reads without tests
+#ifndef DKM_AB_B2_PROBE
+#define DKM_AB_B2_PROBE 0
+#endif
 constexpr int SB2 = DKM_AB_SB2;
 constexpr uint32_t PACK2 = 9, PACK2_MASK = (1u << PACK2) - 1;
 constexpr int B2_ENT = 3;    // kept (score, centre) per sample besides p
 constexpr int B2_RTHR = 4;   // over-full samples a wave tolerates per tile
-// per-wave LDS scratch: -T[32], hint[32], count[32], entries[32][B2_ENT],
-// then 32 x nkw own-mask words
-constexpr int B2_SCR_FIXED = 3 * 128 + 32 * B2_ENT * 8;
+// per-wave LDS scratch: -T[32], hint[32], count[32], |x|^2[32], the tile
+// transpose (32 rows x 16 bf16 features, 1 KB; the kept entries
+// [32][B2_ENT] reuse it after the tile's conversion), then 32 x nkw
+// own-mask words
+constexpr int B2_SCR_FIXED = 4 * 128 + 1024;
+static_assert(32 * B2_ENT * 8 <= 1024, "kept entries fit the transpose");
+
+// v_min3 / v_min without fminf's NaN canonicalisation (inline asm: the
+// compiler would insert v_max_f32 x, x on every MFMA result)
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmin2(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -64,10 +85,21 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// the workspace pointers the kernel reads (the whole WsView as a kernel
+// argument kept ~60 SGPRs of unused pointers live: 82 SGPRs spilled)
+struct B2View {
+  WsHeader *hdr;
+  const uint16_t *b1frag;
+  const float *cn32f, *cn32;
+  int2 *tlist, *clist;
+  int4 *nlist;
+  int32_t *tcount, *ccount, *ncount;
+};
+
 template <class TX, int NKS, bool W1>
 __global__ void __launch_bounds__(SB2)
     k_screen_b2(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
-                WsView v, int32_t *__restrict__ lab_out, int64_t base,
+                B2View v, int32_t *__restrict__ lab_out, int64_t base,
                 int delta, int hint) {
   typedef float f32x16 __attribute__((ext_vector_type(16)));
   constexpr int GB = 1 << (PACK2 - 4);  // 32-centre blocks per top-3 group
@@ -113,7 +145,9 @@ __global__ void __launch_bounds__(SB2)
   float *s_tn = (float *)scr;              // -T per sample
   int *s_hp = (int *)(scr + 128);          // hint per sample (-1: none)
   int *s_cnt = (int *)(scr + 256);         // kept entries appended
-  int2 *s_ent = (int2 *)(scr + 384);       // (score bits, centre)
+  float *s_xx = (float *)(scr + 384);      // |x|^2 per sample
+  char *s_tx = scr + 512;                   // one K-step of the tile, bf16
+  int2 *s_ent = (int2 *)(scr + 512);       // (score bits, centre), later
   uint32_t *s_om = (uint32_t *)(scr + B2_SCR_FIXED);  // [word][column]
   int2 *wl = v.tlist + wv * TL_CAP;  // >= 3 candidates
   int2 *cl = v.clist + wv * B1_CAP;  // 2 candidates
@@ -123,10 +157,32 @@ __global__ void __launch_bounds__(SB2)
   int tl_cnt = 0, cl_cnt = 0, tl_over = 0;
   uint32_t t_tiles = 0, t_done = 0;  // threshold passes run / accepted
 
-  double tile[NKS][8];
+  // ---- tile loads: whole 128-B lines per wave-instruction ----------------
+  // A lane's MFMA operand is 8 features of ITS sample, so loading it
+  // directly touches 32 rows (64 lines) per wave-instruction: that pattern
+  // streamed X at 3.4 TB/s (d = 64) against 6.0 TB/s for whole lines
+  // (tools/membench.hip, profiles/r03/membench.txt).  Here K-step ks of
+  // the tile (16 features = one 128-B line per fp64 row) is read by lanes
+  // l = (row RI i + l / LR, 16-B piece l % LR): RI rows per instruction, every
+  // line whole.  Each lane converts its piece to bf16 and the K-step goes
+  // through a 1 KB LDS transpose into the operand layout; |x|^2 is summed
+  // by the loading lanes (same rows for every K-step) and handed over the
+  // same way.
+  constexpr int EPL = 16 / (int)sizeof(TX);  // elements per 16-B piece
+  constexpr int LR = 16 / EPL;                // lanes per row line (8 | 4)
+  constexpr int RI = 64 / LR;                 // rows per instruction (8 | 16)
+  constexpr int IC = 32 / RI;                 // instructions per K-step (4 | 2)
+  typedef TX tx4 __attribute__((ext_vector_type(EPL)));
+  tx4 raw[NKS][IC];
   int pv = -1;
-  const uint32_t lane_off = (uint32_t)(r * ldx * (int64_t)sizeof(TX)) +
-                            (uint32_t)(8 * h * sizeof(TX));
+  const int lrow = lane / LR, lpos = lane % LR;
+  // per-instruction lane offsets (VGPRs; the K-step offset rides in the
+  // instruction's immediate): as SGPR soffsets they were 4 NKS live SGPRs
+  uint32_t lane_off[IC];
+#pragma unroll
+  for (int i = 0; i < IC; ++i)
+    lane_off[i] = (uint32_t)((RI * i + lrow) * ldx * (int64_t)sizeof(TX)) +
+                  (uint32_t)(16 * lpos);
   auto load_tile = [&](int64_t s0) {
     const int64_t rows = std::max<int64_t>(0, n - s0);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
@@ -139,64 +195,77 @@ __global__ void __launch_bounds__(SB2)
           (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
       pv = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
     }
-    // all of the tile's loads unconditionally (one wait covers them); rows
-    // past n read 0 (num_records), features past d are zeroed below
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const int o = 16 * ks * (int)sizeof(TX);
-      if constexpr (sizeof(TX) == 8) {
-#pragma unroll
-        for (int p4 = 0; p4 < 4; ++p4) {
-          const double2 v2 = __builtin_bit_cast(
-              double2, __builtin_amdgcn_raw_buffer_load_b128(
-                           rx, lane_off, o + 16 * p4, 0));
-          tile[ks][2 * p4] = v2.x;
-          tile[ks][2 * p4 + 1] = v2.y;
-        }
-      } else {
-#pragma unroll
-        for (int p4 = 0; p4 < 2; ++p4) {
-          const float4 v4 = __builtin_bit_cast(
-              float4, __builtin_amdgcn_raw_buffer_load_b128(
-                          rx, lane_off, o + 16 * p4, 0));
-          tile[ks][4 * p4] = v4.x;
-          tile[ks][4 * p4 + 1] = v4.y;
-          tile[ks][4 * p4 + 2] = v4.z;
-          tile[ks][4 * p4 + 3] = v4.w;
-        }
-      }
-    }
-    if (d != 16 * NKS) {  // wave-uniform
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-          tile[ks][m] = 16 * ks + 8 * h + m < d ? tile[ks][m] : 0.0;
-    }
-  };
-
-  for (int64_t s0 = base + wv * 32; s0 < n; s0 += step) {
-    load_tile(s0);
-    float xx = 0.f;
-    bf16x8 xh[NKS];
+    // every load issued before the first use; rows past n read 0
+    // (num_records), features past d are zeroed at conversion
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
-      for (int m = 0; m < 8; m += 2) {
-        const float x0 = (float)tile[ks][m];
-        const float x1 = (float)tile[ks][m + 1];
-        xx = fmaf(x0, x0, xx);
-        xx = fmaf(x1, x1, xx);
-        const bf16x2 h2 = __builtin_convertvector(f32x2{x0, x1}, bf16x2);
-        xh[ks][m] = h2[0];
-        xh[ks][m + 1] = h2[1];
+      for (int i = 0; i < IC; ++i)
+        raw[ks][i] = __builtin_bit_cast(
+            tx4, __builtin_amdgcn_raw_buffer_load_b128(
+                     rx, lane_off[i] + 16 * ks * (int)sizeof(TX), 0, 0));
+  };
+  // operand half of row `row` in the transpose: swizzled by (row >> 3) & 1
+  // so that the ds_read_b128 lane groups hit 64 distinct banks
+  auto tx_addr = [](int row, int half) {
+    return 32 * row + 16 * (half ^ ((row >> 3) & 1));
+  };
+
+  // A/B (-DDKM_AB_B2_PF=1, pair with -DDKM_AB_SB2=512): the next tile's
+  // loads are issued as soon as this one is converted
+#ifndef DKM_AB_B2_PF
+#define DKM_AB_B2_PF 0
+#endif
+  if (DKM_AB_B2_PF && base + wv * 32 < n) load_tile(base + wv * 32);
+  for (int64_t s0 = base + wv * 32; s0 < n; s0 += step) {
+    if (!DKM_AB_B2_PF) load_tile(s0);
+    bf16x8 xh[NKS];
+    float xp[IC];  // |x|^2 partials of rows RI i + lrow
+#pragma unroll
+    for (int i = 0; i < IC; ++i) xp[i] = 0.f;
+    // features past d (d % 16 != 0): lim recomputed per tile (opaque), or
+    // the lane masks are hoisted into long-lived SGPR pairs
+    const int lim = d == 16 * NKS ? 0x7fffffff
+                                  : (int)opaque_u32((uint32_t)(d - EPL * lpos));
+    wave_sync();  // the previous tile's kept entries were read
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+      for (int i = 0; i < IC; ++i) {
+        float xf[EPL];
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          const float x = (float)raw[ks][i][e];
+          xf[e] = 16 * ks + e < lim ? x : 0.f;
+          xp[i] = fmaf(xf[e], xf[e], xp[i]);
+        }
+        const int row = RI * i + lrow;
+        if constexpr (EPL == 2) {
+          const bf16x2 b2 = __builtin_convertvector(f32x2{xf[0], xf[1]}, bf16x2);
+          *(bf16x2 *)(s_tx + tx_addr(row, lpos >> 2) + 4 * (lpos & 3)) = b2;
+        } else {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          const bf16x2 a2 = __builtin_convertvector(f32x2{xf[0], xf[1]}, bf16x2);
+          const bf16x2 b2 = __builtin_convertvector(f32x2{xf[2], xf[3]}, bf16x2);
+          *(bf16x4 *)(s_tx + tx_addr(row, lpos >> 1) + 8 * (lpos & 1)) =
+              bf16x4{a2[0], a2[1], b2[0], b2[1]};
+        }
       }
-    {
-      float xa, xb;
-      pair_xor<32>(xx, xa, xb);
-      xx = xa + xb;
+      wave_sync();
+      xh[ks] = *(const bf16x8 *)(s_tx + tx_addr(r, h));
+      wave_sync();
     }
+    // |x|^2: the LR lanes of a row line hold its partials
+#pragma unroll
+    for (int i = 0; i < IC; ++i) {
+#pragma unroll
+      for (int m = 1; m < LR; m <<= 1) xp[i] += __shfl_xor(xp[i], m, 64);
+      if (lpos == 0) s_xx[RI * i + lrow] = xp[i];
+    }
+    wave_sync();
+    const float xx = s_xx[r];
     const int prv = pv;
+    if (DKM_AB_B2_PF && s0 + step < n) load_tile(s0 + step);
     const int64_t si = s0 + r;
     float xn;
     const float B2 = bound2_fast(bk, xx, xn);
@@ -229,10 +298,25 @@ __global__ void __launch_bounds__(SB2)
         }
         // diagonal: row r sits in half (r >> 2) & 1, register
         // (r & 3) + 4 (r >> 3); the other lane of the pair contributes 0
-        const int gsel = h == ((r >> 2) & 1) ? (r & 3) + 4 * (r >> 3) : -1;
-        float dg = 0.f;
+        // two-level select (register group r >> 3, then slot r & 3): 15
+        // v_cndmask on 6 lane masks, recomputed per tile (opaque) so that
+        // they are not hoisted into long-lived SGPR pairs
+        float dg;
+        {
+          const int rr = (int)opaque_u32((uint32_t)r);
+          const int q = rr >> 3, w = rr & 3;
+          float sl[4];
 #pragma unroll
-        for (int g = 0; g < 16; ++g) dg = gsel == g ? dn[g] : dg;
+          for (int t = 0; t < 4; ++t) {
+            float x = dn[t];
+            x = q == 1 ? dn[4 + t] : x;
+            x = q == 2 ? dn[8 + t] : x;
+            x = q == 3 ? dn[12 + t] : x;
+            sl[t] = x;
+          }
+          dg = w == 0 ? sl[0] : w == 1 ? sl[1] : w == 2 ? sl[2] : sl[3];
+          dg = h == ((rr >> 2) & 1) ? dg : 0.f;
+        }
         {
           float da, db;
           pair_xor<32>(dg, da, db);
@@ -299,13 +383,13 @@ __global__ void __launch_bounds__(SB2)
           }
         }
         // ---- all centre blocks: lane = centre, registers = samples -------
-        auto rd = [&](int cb, bf16x8 (&f)[NKS], float &nc) {
+        auto rd_f = [&](int cb, bf16x8 (&f)[NKS]) {
 #pragma unroll
           for (int ks = 0; ks < NKS; ++ks)
             f[ks] = *(const bf16x8 *)(frag + ((int64_t)cb * NKS + ks) * 1024 +
                                       lane * 16);
-          nc = ncn[cb * 32 + r];
         };
+        auto rd_n = [&](int cb) { return ncn[cb * 32 + r]; };
         auto mm = [&](const bf16x8 (&f)[NKS], f32x16 &acc) {
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[0], f[0], cin, 0, 0,
                                                         0);
@@ -322,14 +406,18 @@ __global__ void __launch_bounds__(SB2)
           const int own = (int)(w << (31 - (cb & 31))) >> 31;
           thr = __uint_as_float(((uint32_t)own & 0xff800000u) |
                                 __float_as_uint(nc));
-          float mp[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            mp[i] = __builtin_amdgcn_fmed3f(acc[2 * i], acc[2 * i + 1], ninf);
-          const float a = fminf(fminf(mp[0], mp[1]), mp[2]);
-          const float b = fminf(fminf(mp[3], mp[4]), mp[5]);
-          const float c = fminf(fminf(mp[6], mp[7]), a);
-          any = fminf(b, c) <= thr;
+          // 7 v_min3 + 1 v_min on the raw MFMA results (no NaN
+          // canonicalisation: a NaN score comes with a NaN threshold, and
+          // its sample is rejected by the `sane` test)
+          const float m0 = vmin3(acc[0], acc[1], acc[2]);
+          const float m1 = vmin3(acc[3], acc[4], acc[5]);
+          const float m2 = vmin3(acc[6], acc[7], acc[8]);
+          const float m3 = vmin3(acc[9], acc[10], acc[11]);
+          const float m4 = vmin3(acc[12], acc[13], acc[14]);
+          const float m5 = vmin3(m0, m1, m2);
+          const float m6 = vmin3(m3, m4, acc[15]);
+          any = vmin2(m5, m6) <= thr;
+          if (DKM_AB_B2_PROBE == 2) any = acc[0] == 12345.f;  // (invalid)
         };
         auto append = [&](int cb, const f32x16 &acc, float thr, float nc,
                           bool any) {
@@ -341,42 +429,52 @@ __global__ void __launch_bounds__(SB2)
                 push((g & 3) + 8 * (g >> 2) + 4 * h, (acc[g] - cin[g]) - nc, j);
           }
         };
-        {
+        if (DKM_AB_B2_PROBE != 1) {
+          // software pipeline, one block deep: block t's chain is issued
+          // before block t - 1 is tested (the test VALU overlaps the MFMA
+          // chain instead of waiting for its own block's results), and the
+          // fragments of t + 1 are read while t's chain runs
           f32x16 acc_a, acc_b;
           bf16x8 fa[NKS], fb[NKS];
           float na, nb, ta, tb;
           bool ga, gb;
-          auto interleave = [&]() {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1 + NKS, 0);  // DS rd
-#pragma unroll
-            for (int i = 0; i < NKS; ++i) {
-              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-              __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
-            }
-          };
-          rd(0, fa, na);
-          mm(fa, acc_a);
-          int cb = 0;
-          for (; cb + 2 < nkb; cb += 2) {
-            rd(cb + 1, fb, nb);
-            test(cb, acc_a, na, ta, ga);
-            mm(fb, acc_b);
-            interleave();
-            append(cb, acc_a, ta, na, ga);
-            rd(cb + 2, fa, na);
-            test(cb + 1, acc_b, nb, tb, gb);
-            mm(fa, acc_a);
-            interleave();
-            append(cb + 1, acc_b, tb, nb, gb);
+          rd_f(0, fa);
+          na = rd_n(0);
+          mm(fa, acc_a);  // chain 0
+          if (nkb > 1) {
+            rd_f(1, fb);
+            nb = rd_n(1);
           }
-          if (cb + 1 < nkb) {
-            rd(cb + 1, fb, nb);
+          int cb = 0;
+          // steady state: chains cb + 1, cb + 2 and reads cb + 2, cb + 3
+          for (; cb + 3 < nkb; cb += 2) {
+            mm(fb, acc_b);  // chain cb + 1
+            rd_f(cb + 2, fa);
             test(cb, acc_a, na, ta, ga);
-            mm(fb, acc_b);
-            interleave();
             append(cb, acc_a, ta, na, ga);
+            na = rd_n(cb + 2);
+            mm(fa, acc_a);  // chain cb + 2
+            rd_f(cb + 3, fb);
             test(cb + 1, acc_b, nb, tb, gb);
             append(cb + 1, acc_b, tb, nb, gb);
+            nb = rd_n(cb + 3);
+          }
+          // tail: 1, 2 or 3 blocks left (chain cb issued, reads cb + 1 done)
+          if (cb + 1 < nkb) {
+            mm(fb, acc_b);  // chain cb + 1
+            if (cb + 2 < nkb) rd_f(cb + 2, fa);
+            test(cb, acc_a, na, ta, ga);
+            append(cb, acc_a, ta, na, ga);
+            if (cb + 2 < nkb) {
+              na = rd_n(cb + 2);
+              mm(fa, acc_a);  // chain cb + 2
+            }
+            test(cb + 1, acc_b, nb, tb, gb);
+            append(cb + 1, acc_b, tb, nb, gb);
+            if (cb + 2 < nkb) {
+              test(cb + 2, acc_a, na, ta, ga);
+              append(cb + 2, acc_a, ta, na, ga);
+            }
           } else {
             test(cb, acc_a, na, ta, ga);
             append(cb, acc_a, ta, na, ga);
@@ -598,6 +696,8 @@ size_t b2_lds_bytes(int64_t k, int64_t d) {
 
 // DKM_B1_LEGACY=1 runs k_screen_b1 instead (A/B and its parity tests); read
 // per launch so that one process can run both
+int b2_probe() { return DKM_AB_B2_PROBE; }
+
 bool b2_enabled() {
   const char *e = getenv("DKM_B1_LEGACY");
   return !(e && *e && *e != '0');
@@ -633,15 +733,26 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
   *nseg = (int)std::min<int64_t>((int64_t)g * (SB2 / 64),
                                  std::min(TL_SEGS, B1_SEGS));
   const int delta = 0;  // labels only (the sums come from the labels)
+  B2View bv;
+  bv.hdr = v.hdr;
+  bv.b1frag = v.b1frag;
+  bv.cn32f = v.cn32f;
+  bv.cn32 = v.cn32;
+  bv.tlist = v.tlist;
+  bv.clist = v.clist;
+  bv.nlist = v.nlist;
+  bv.tcount = v.tcount;
+  bv.ccount = v.ccount;
+  bv.ncount = v.ncount;
   switch (nks) {
 #define DKM_B2L(N)                                                      \
   case N:                                                               \
     if (w1)                                                             \
       k_screen_b2<TX, N, true><<<g, SB2, lds, s>>>(                     \
-          X, end, d, ldx, k, v, lab_out, base, delta, hint);            \
+          X, end, d, ldx, k, bv, lab_out, base, delta, hint);           \
     else                                                                \
       k_screen_b2<TX, N, false><<<g, SB2, lds, s>>>(                    \
-          X, end, d, ldx, k, v, lab_out, base, delta, hint);            \
+          X, end, d, ldx, k, bv, lab_out, base, delta, hint);           \
     break;
     DKM_B2L(1) DKM_B2L(2) DKM_B2L(3) DKM_B2L(4)
     DKM_B2L(5) DKM_B2L(6) DKM_B2L(7) DKM_B2L(8)

@@ -947,6 +947,12 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
 // argument and the same list / label / accumulation contract as k_screen.
 // ---------------------------------------------------------------------------
 constexpr int SBW = 256;  // k_screen_w32 block: 4 waves, 3 blocks per CU
+constexpr int W32_SCR = 2048 + 128 + 128;  // per-wave LDS scratch
+__device__ __forceinline__ void wave_sync_w() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 // cache policy of k_screen_w32's streaming row loads (0 = default; 2 = NT)
 #ifndef DKM_XLOAD_AUX
 #define DKM_XLOAD_AUX 0
@@ -985,6 +991,15 @@ __global__ void __launch_bounds__(SBW) __attribute__((
 
   const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // per-wave scratch (W32_SCR bytes) after the accumulators: the transpose
+  // of one 16-feature half of the tile (bf16 hi then lo, 32 rows x 32 B
+  // each), |x|^2 per sample, the decided labels (full sums)
+  char *scr = (char *)((amode & AM_INLDS) ? lds_acc + lds_acc_len(k, d)
+                                          : lds_acc) +
+              wid * W32_SCR;
+  char *s_hi = scr, *s_lo = scr + 1024;
+  float *s_xx = (float *)(scr + 2048);
+  int *s_lab = (int *)(scr + 2176);
   const int64_t wv = (int64_t)blockIdx.x * (SBW / 64) + wid;
   const int64_t step = (int64_t)gridDim.x * (SBW / 64) * 32;
   const int64_t seg = wv;
@@ -992,10 +1007,28 @@ __global__ void __launch_bounds__(SBW) __attribute__((
   const bool listing = use_list && seg < TL_SEGS;
   int tl_cnt = 0, tl_over = 0;
 
-  double tile[16];
+  // Whole 128-B lines per wave-instruction (tools/membench.hip: loading
+  // each lane's own 16 features touched 64 lines per instruction and
+  // streamed X at 3.9 TB/s; whole lines 6.2 TB/s).  Half c of the tile
+  // (features 16c .. 16c + 15, one line per fp64 row) is read by lanes
+  // l = (row RI i + l / LR, 16-B piece l % LR); the lanes convert their
+  // pieces to bf16 hi + lo, and the half reaches its consumer lanes
+  // (h = c) through a 2 KB LDS transpose.  The loading lanes keep the raw
+  // values for the full sums and sum |x|^2 of their rows.
+  constexpr int EPL = 16 / (int)sizeof(TX);  // elements per 16-B piece
+  constexpr int LR = 16 / EPL;                // lanes per row line (8 | 4)
+  constexpr int RI = 64 / LR;                 // rows per instruction
+  constexpr int IC = 32 / RI;                 // instructions per half
+  typedef TX txv __attribute__((ext_vector_type(EPL)));
+  txv raw[2][IC];
   int pv = -1;
-  const uint32_t lane_off = (uint32_t)(r * ldx * (int64_t)sizeof(TX)) +
-                            (uint32_t)(16 * h * sizeof(TX));
+  const int lrow = lane / LR, lpos = lane % LR;
+  uint32_t lane_off[IC];
+#pragma unroll
+  for (int i = 0; i < IC; ++i)
+    lane_off[i] = (uint32_t)((RI * i + lrow) * ldx * (int64_t)sizeof(TX)) +
+                  (uint32_t)(16 * lpos);
+  const bool two = d > 16;  // the second half holds features
   auto load_tile = [&](int64_t s0) {
     const int64_t rows = std::max<int64_t>(0, n - s0);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
@@ -1009,67 +1042,80 @@ __global__ void __launch_bounds__(SBW) __attribute__((
       pv = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
     }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      if (16 * h + 8 * ks < d) {
-        // one lane offset register; the constant part rides in soffset
-        const int o = 8 * ks * (int)sizeof(TX);
-        if constexpr (sizeof(TX) == 8) {
+    for (int c = 0; c < 2; ++c)
 #pragma unroll
-          for (int p4 = 0; p4 < 4; ++p4) {
-            const double2 v2 = __builtin_bit_cast(
-                double2, __builtin_amdgcn_raw_buffer_load_b128(
-                             rx, lane_off, o + 16 * p4, DKM_XLOAD_AUX));
-            tile[8 * ks + 2 * p4] = v2.x;
-            tile[8 * ks + 2 * p4 + 1] = v2.y;
-          }
-        } else {
-#pragma unroll
-          for (int p4 = 0; p4 < 2; ++p4) {
-            const float4 v4 = __builtin_bit_cast(
-                float4, __builtin_amdgcn_raw_buffer_load_b128(
-                            rx, lane_off, o + 16 * p4, DKM_XLOAD_AUX));
-            tile[8 * ks + 4 * p4] = v4.x;
-            tile[8 * ks + 4 * p4 + 1] = v4.y;
-            tile[8 * ks + 4 * p4 + 2] = v4.z;
-            tile[8 * ks + 4 * p4 + 3] = v4.w;
-          }
+      for (int i = 0; i < IC; ++i) {
+        if (c == 1 && !two) {
+          raw[c][i] = txv{};
+          continue;
         }
-      } else {
-#pragma unroll
-        for (int m = 0; m < 8; ++m) tile[8 * ks + m] = 0.0;
+        raw[c][i] = __builtin_bit_cast(
+            txv, __builtin_amdgcn_raw_buffer_load_b128(
+                     rx, lane_off[i] + 16 * c * (int)sizeof(TX), 0,
+                     DKM_XLOAD_AUX));
       }
-    }
+  };
+  auto tx_addr = [](int row, int q) {  // 16-B quarter q of a 32-B row
+    return 32 * row + 16 * (q ^ ((row >> 3) & 1));
   };
 
   int64_t s0 = base + wv * 32;
   if (s0 < n) load_tile(s0);
   for (; s0 < n; s0 += step) {
-    float xx = 0.f;
     bf16x8 xh[2], xl[2];
+    float xp[IC];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int i = 0; i < IC; ++i) xp[i] = 0.f;
+    // features past d: lim recomputed per tile (opaque), or the lane masks
+    // are hoisted into long-lived SGPR pairs
+    const int lim = (int)opaque_u32((uint32_t)(d - EPL * lpos));
 #pragma unroll
-      for (int m = 0; m < 8; m += 2) {
-        const float x0 = (float)tile[8 * ks + m];
-        const float x1 = (float)tile[8 * ks + m + 1];
-        xx = fmaf(x0, x0, xx);
-        xx = fmaf(x1, x1, xx);
-        const bf16x2 h2 = __builtin_convertvector(f32x2{x0, x1}, bf16x2);
-        const uint32_t hu = __builtin_bit_cast(uint32_t, h2);
-        const float h0 = __uint_as_float(hu << 16);
-        const float h1 = __uint_as_float(hu & 0xffff0000u);
-        const bf16x2 l2 =
-            __builtin_convertvector(f32x2{x0 - h0, x1 - h1}, bf16x2);
-        xh[ks][m] = h2[0];
-        xh[ks][m + 1] = h2[1];
-        xl[ks][m] = l2[0];
-        xl[ks][m + 1] = l2[1];
+    for (int c = 0; c < 2; ++c) {
+      wave_sync_w();  // the previous readers of the transpose are done
+#pragma unroll
+      for (int i = 0; i < IC; ++i) {
+        float xf[EPL];
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          const float x = (float)raw[c][i][e];
+          xf[e] = 16 * c + e < lim ? x : 0.f;
+          xp[i] = fmaf(xf[e], xf[e], xp[i]);
+        }
+        const int row = RI * i + lrow;
+#pragma unroll
+        for (int e = 0; e < EPL; e += 2) {
+          // one v_cvt_pk_bf16_f32 per pair; hi back as fp32 by shift /
+          // mask; lo = x - hi is exact
+          const bf16x2 h2 = __builtin_convertvector(f32x2{xf[e], xf[e + 1]},
+                                                    bf16x2);
+          const uint32_t hu = __builtin_bit_cast(uint32_t, h2);
+          const bf16x2 l2 = __builtin_convertvector(
+              f32x2{xf[e] - __uint_as_float(hu << 16),
+                    xf[e + 1] - __uint_as_float(hu & 0xffff0000u)},
+              bf16x2);
+          // feature 16c + EPL lpos + e: quarter (EPL lpos + e) / 8
+          const int f = EPL * lpos + e;
+          const int o = tx_addr(row, f >> 3) + 2 * (f & 7);
+          *(bf16x2 *)(s_hi + o) = h2;
+          *(bf16x2 *)(s_lo + o) = l2;
+        }
       }
-    {
-      float xa, xb;
-      pair_xor<32>(xx, xa, xb);
-      xx = xa + xb;
+      wave_sync_w();
+      if (h == c) {
+        xh[0] = *(const bf16x8 *)(s_hi + tx_addr(r, 0));
+        xh[1] = *(const bf16x8 *)(s_hi + tx_addr(r, 1));
+        xl[0] = *(const bf16x8 *)(s_lo + tx_addr(r, 0));
+        xl[1] = *(const bf16x8 *)(s_lo + tx_addr(r, 1));
+      }
     }
+#pragma unroll
+    for (int i = 0; i < IC; ++i) {
+#pragma unroll
+      for (int m = 1; m < LR; m <<= 1) xp[i] += __shfl_xor(xp[i], m, 64);
+      if (lpos == 0) s_xx[RI * i + lrow] = xp[i];
+    }
+    wave_sync_w();
+    const float xx = s_xx[r];
     const int prv = pv;
     const int64_t s_next = s0 + step;
     if (!full_acc && s_next < n) load_tile(s_next);
@@ -1154,20 +1200,33 @@ __global__ void __launch_bounds__(SBW) __attribute__((
     } else {
       tl_over += add;
     }
+    if (full_acc) {
+      // the loading lanes add their pieces of the decided rows
+      if (h == 0) s_lab[r] = si < n && unique ? ri : -1;
+      wave_sync_w();
+#pragma unroll
+      for (int i = 0; i < IC; ++i) {
+        const int row = RI * i + lrow;
+        const int lb = s_lab[row];
+        if (lb >= 0) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+              const int t = 16 * c + EPL * lpos + e;
+              if (t < d) at.add(lb, t, (double)raw[c][i][e]);
+            }
+          if (lpos == 0) at.count(lb, 1.0);
+        }
+      }
+    }
     if (si < n) {
       const int lab = ri;
       if (h == 0 && !(unique && lab == prev))
         lab_out[si] = unique ? lab : -(prev + 2);
       if (unique) {
         if (full_acc) {
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-              const int t = 16 * h + 8 * ks + m;
-              if (t < d) at.add(lab, t, tile[8 * ks + m]);
-            }
-          if (h == 0) at.count(lab, 1.0);
+          // added above
         } else if (delta && lab != prev) {
           const TX *xr = X + si * ldx;
 #pragma unroll
@@ -2174,10 +2233,16 @@ __global__ void __launch_bounds__(BLOCK)
 }
 
 __global__ void k_add(double *__restrict__ y, const double *__restrict__ x,
-                      int64_t n) {
+                      int64_t n, int32_t *nz) {
+  bool any = false;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * blockDim.x)
-    y[e] += x[e];
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const double v = x[e];
+    y[e] += v;
+    any |= v != 0.0;
+  }
+  // one store per wave that saw a nonzero (the flag was zeroed before)
+  if (nz && __ballot(any) && (threadIdx.x & 63) == 0) nz[0] = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -2280,6 +2345,7 @@ static int launch_screen_w32(const TX *X, int64_t end, int d, int64_t ldx,
                              double *acc, int amode, int64_t base, size_t lds,
                              int use_list, hipStream_t s, int *nseg) {
   const void *kf = (const void *)k_screen_w32<TX>;
+  lds += (size_t)(SBW / 64) * W32_SCR;  // the waves' transpose scratch
   const int64_t cap = (int64_t)dev_info().cus * resident_blocks(kf, SBW, lds);
   const int64_t per_block = 32 * (SBW / 64);
   const int64_t need = (end - base + per_block - 1) / per_block;
@@ -2872,8 +2938,20 @@ int dkm_add_f64(double *y, const double *x, int64_t n, void *stream) {
   if ((!y || !x) && n > 0) return fail(DKM_E_ARG, "add: NULL");
   if (n <= 0) return 0;
   const int64_t g = std::min<int64_t>((n + 255) / 256, 4096);
-  k_add<<<(unsigned)g, 256, 0, (hipStream_t)stream>>>(y, x, n);
+  k_add<<<(unsigned)g, 256, 0, (hipStream_t)stream>>>(y, x, n, nullptr);
   return check_launch("dkm_add_f64");
+}
+
+int dkm_add_f64_nz(double *y, const double *x, int64_t n, int32_t *nonzero,
+                   void *stream) {
+  if ((!y || !x) && n > 0) return fail(DKM_E_ARG, "add_nz: NULL");
+  if (!nonzero) return fail(DKM_E_ARG, "add_nz: NULL flag");
+  if (hipMemsetAsync(nonzero, 0, 4, (hipStream_t)stream) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "add_nz: flag reset");
+  if (n <= 0) return 0;
+  const int64_t g = std::min<int64_t>((n + 255) / 256, 4096);
+  k_add<<<(unsigned)g, 256, 0, (hipStream_t)stream>>>(y, x, n, nonzero);
+  return check_launch("dkm_add_f64_nz");
 }
 
 // Result-invalidating A/B timing probes (variants.sh builds only): the
@@ -2883,7 +2961,7 @@ int dkm_build_flags(void) {
 #if DKM_AB_B1_PROBE || defined(DKM_DBG_NOCOMPUTE) || defined(DKM_DBG_NOLOAD)
   return DKM_BUILD_TIMING_ONLY;
 #else
-  return 0;
+  return b2_probe() ? DKM_BUILD_TIMING_ONLY : 0;
 #endif
 }
 

@@ -143,6 +143,7 @@ struct WsView {
 // threshold pass without per-block norm reads.  Returns 1 (nothing
 // launched) when its LDS image does not fit; the caller runs k_screen_b1.
 bool b2_enabled();
+int b2_probe();  // != 0: a result-invalidating timing probe build
 size_t b2_lds_bytes(int64_t k, int64_t d);
 template <class TX>
 int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,

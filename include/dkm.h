@@ -114,6 +114,13 @@ int dkm_assign_delta_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
 
 /* y[i] += x[i] (device, fp64): acc_new = acc_old + delta.                  */
 int dkm_add_f64(double *y, const double *x, int64_t n, void *stream);
+/* The same, and *nonzero (device int32) <- 1 if any x[i] != 0, else 0:
+ * a delta of all zeros leaves acc bit-identical, so the caller knows that
+ * no sample changed cluster since its last full recomputation (its
+ * periodic refresh is then skipped: the sums are exactly those of the
+ * current assignment).                                                   */
+int dkm_add_f64_nz(double *y, const double *x, int64_t n, int32_t *nonzero,
+                   void *stream);
 
 /* Assignment only.  Replaces `_predict` (base.py:194-201).  Needs a prepared
  * workspace (dkm_prepare_centers with acc = NULL is allowed).             */

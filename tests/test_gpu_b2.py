@@ -164,3 +164,40 @@ def test_threshold_pass_tail_and_hint_edge_cases(variant):
     lab, sums, cnt = _hinted(x, C, hint)
     assert np.array_equal(lab, rl)
     assert np.array_equal(cnt, rc.astype(np.float64))
+
+
+def test_refresh_skipped_once_converged(monkeypatch):
+    """The periodic full recomputation of the running sums is skipped when
+    no delta since the last one moved a sample (the sums are then exactly
+    those of the current assignment): a fit that converges early makes
+    fewer full passes than it < max_iter / REFRESH, and still matches the
+    oracle (labels bit-exact, centres 1e-9, n_iter)."""
+    from sklearn.datasets import make_blobs
+
+    import dislib_amd.cluster.kmeans as km_mod
+    from dislib_amd import _device
+    from dislib_amd.cluster import KMeans
+    from dislib_amd.data import load_data
+    x, _ = make_blobs(n_samples=20000, n_features=64, centers=200,
+                      center_box=(-10, 10), random_state=4)
+    ref = orc.OracleKMeans(n_clusters=200, max_iter=14, tol=0,
+                           random_state=0)
+    rl = ref.fit([x[i:i + 5000] for i in range(0, 20000, 5000)],
+                 set_labels=True)
+    calls = []
+    real = _device.partial_sum
+
+    def counted(*a, **kw):
+        calls.append(1)
+        return real(*a, **kw)
+    monkeypatch.setattr(_device, "partial_sum", counted)
+    monkeypatch.setattr(km_mod, "REFRESH", 2)
+    ds = load_data(x, 5000)
+    km = KMeans(n_clusters=200, max_iter=14, tol=0, random_state=0)
+    km.fit_predict(ds)
+    assert km.n_iter == ref.n_iter
+    assert np.array_equal(ds.labels_int32(), rl)
+    err = np.max(np.abs(km.centers - ref.centers) /
+                 np.maximum(np.abs(ref.centers), 1.0))
+    assert err <= 1e-9
+    assert 1 <= len(calls) < 7, len(calls)

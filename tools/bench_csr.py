@@ -50,7 +50,7 @@ def main():
         st.prepare()
         st.partial()
         st.reduce_update()
-        st.flag.item()
+        st.read_flags()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     # one full (refresh) assignment + sums, and predict, timed alone
