@@ -12,10 +12,17 @@ per-task pickling of Subsets (reference ``cluster/kmeans/base.py:113-115``,
 for every Lloyd iteration.
 """
 import ctypes
+import os
 
 import numpy as np
 
 from . import _lib
+
+# DKM_X_IMAGE=0: never build the sample image (the screen then converts X
+# itself; identical labels -- A/B and parity runs)
+X_IMAGE = os.environ.get("DKM_X_IMAGE", "1") != "0"
+# HBM left free after an image is allocated
+_IMAGE_HEADROOM = 4 << 30
 
 
 def torch():
@@ -54,8 +61,11 @@ def ptr(t):
 class DeviceData:
     """HBM image of a Dataset (dense or CSR)."""
 
+    image = None          # the sample image (screen_image)
+
     def __init__(self, dataset, device=None):
         self.device = resolve(device)
+        self._image_failed = False
         subsets = list(dataset)
         self.sizes = [int(s.samples.shape[0]) for s in subsets]
         self.offsets = np.concatenate([[0], np.cumsum(self.sizes)]).astype(
@@ -115,6 +125,35 @@ class DeviceData:
         self.indices = t.from_numpy(m.indices.astype(np.int32)).to(
             self.device)
         self.data = t.from_numpy(m.data.astype(np.float64)).to(self.device)
+
+    # -- the sample image ---------------------------------------------------
+    def screen_image(self, k, mode):
+        """The resident bf16 operand image of X (dkm_x_image_*) when the
+        screen that (k, d, mode) selects reads one; built on first use
+        (stream-ordered, one pass over X) and kept with the data, which is
+        immutable.  None when not useful, disabled (DKM_X_IMAGE=0) or when
+        it would leave less than 4 GiB of HBM free."""
+        if self.sparse or not X_IMAGE or self.n == 0:
+            return None
+        if self.image is not None:
+            return self.image
+        so = _lib.lib()
+        if self._image_failed or not so.dkm_x_image_useful(int(k), self.d,
+                                                           int(mode)):
+            return None
+        t = torch()
+        nb = int(so.dkm_x_image_bytes(self.n, self.d))
+        free = t.cuda.mem_get_info(self.device)[0]
+        if nb == 0 or nb + _IMAGE_HEADROOM > free:
+            self._image_failed = True
+            return None
+        img = t.empty(nb, dtype=t.uint8, device=self.device)
+        fn = so.dkm_x_image_f32 if self.dtype == np.float32 else \
+            so.dkm_x_image_f64
+        _lib.check(fn(ptr(self.X), self.n, self.d, self.X.stride(0), ptr(img),
+                      nb, stream_ptr()), "dkm_x_image")
+        self.image = img
+        return img
 
     # -- helpers -----------------------------------------------------------
     def subset_slices(self):
@@ -189,6 +228,14 @@ def partial_sum(dd, C, ws, labels, acc, mode):
             ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(acc), stream_ptr()),
             "dkm_partial_sum_csr_f64")
         return
+    img = dd.screen_image(k, mode) if labels is not None else None
+    if img is not None:
+        fn = so.dkm_partial_sum_img_f32 if dd.dtype == np.float32 else \
+            so.dkm_partial_sum_img_f64
+        _lib.check(fn(ptr(dd.X), ptr(img), dd.n, dd.d, dd.X.stride(0),
+                      ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(acc), mode,
+                      stream_ptr()), "dkm_partial_sum_img")
+        return
     fn = so.dkm_partial_sum_f32 if dd.dtype == np.float32 else \
         so.dkm_partial_sum_f64
     _lib.check(fn(ptr(dd.X), dd.n, dd.d, dd.X.stride(0), ptr(C), k, ws.p,
@@ -205,6 +252,14 @@ def assign_delta(dd, C, ws, labels, delta, mode):
             ptr(dd.indptr), ptr(dd.indices), ptr(dd.data), dd.n, dd.d,
             ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(delta),
             stream_ptr()), "dkm_assign_delta_csr_f64")
+        return
+    img = dd.screen_image(k, mode)
+    if img is not None:
+        fn = so.dkm_assign_delta_img_f32 if dd.dtype == np.float32 else \
+            so.dkm_assign_delta_img_f64
+        _lib.check(fn(ptr(dd.X), ptr(img), dd.n, dd.d, dd.X.stride(0),
+                      ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(delta),
+                      mode, stream_ptr()), "dkm_assign_delta_img")
         return
     fn = so.dkm_assign_delta_f32 if dd.dtype == np.float32 else \
         so.dkm_assign_delta_f64

@@ -38,6 +38,18 @@ SIGNATURES = {
                                     _p, _p, _i32, _p]),
     "dkm_assign_delta_f32": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz,
                                     _p, _p, _i32, _p]),
+    "dkm_x_image_bytes": (_sz, [_i64, _i64]),
+    "dkm_x_image_useful": (_i32, [_i64, _i64, _i32]),
+    "dkm_x_image_f64": (_i32, [_p, _i64, _i64, _i64, _p, _sz, _p]),
+    "dkm_x_image_f32": (_i32, [_p, _i64, _i64, _i64, _p, _sz, _p]),
+    "dkm_partial_sum_img_f64": (_i32, [_p, _p, _i64, _i64, _i64, _p, _i64,
+                                       _p, _sz, _p, _p, _i32, _p]),
+    "dkm_partial_sum_img_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _i64,
+                                       _p, _sz, _p, _p, _i32, _p]),
+    "dkm_assign_delta_img_f64": (_i32, [_p, _p, _i64, _i64, _i64, _p, _i64,
+                                        _p, _sz, _p, _p, _i32, _p]),
+    "dkm_assign_delta_img_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _i64,
+                                        _p, _sz, _p, _p, _i32, _p]),
     "dkm_add_f64": (_i32, [_p, _p, _i64, _p]),
     "dkm_add_f64_nz": (_i32, [_p, _p, _i64, _p, _p]),
     "dkm_predict_f64": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz, _p,

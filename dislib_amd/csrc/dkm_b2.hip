@@ -64,6 +64,17 @@ constexpr int B2_RTHR = 4;   // over-full samples a wave tolerates per tile
 // [32][B2_ENT] reuse it after the tile's conversion), then 32 x nkw
 // own-mask words
 constexpr int B2_SCR_FIXED = 4 * 128 + 1024;
+// producer/consumer form (PC): B2_NLOAD loader waves (one per SIMD) stream
+// tiles through a ring of B2_S LDS slots (bf16 tile in the operand layout,
+// |x|^2, hints) to the consumer waves, which claim tiles in order from an
+// LDS counter.  Consumer scratch: -T, hints, counts, (|x|^2 unused), kept
+// entries, own masks.
+constexpr int B2_NLOAD = 4;
+constexpr int B2_S = 3;
+constexpr int B2_CSCR = 4 * 128 + 32 * B2_ENT * 8;
+__host__ __device__ constexpr int b2_slot_bytes(int nks) {
+  return nks * 1024 + 256;
+}
 static_assert(32 * B2_ENT * 8 <= 1024, "kept entries fit the transpose");
 
 // v_min3 / v_min without fminf's NaN canonicalisation (inline asm: the
@@ -96,11 +107,11 @@ struct B2View {
   int32_t *tcount, *ccount, *ncount;
 };
 
-template <class TX, int NKS, bool W1>
+template <class TX, int NKS, bool W1, bool PC, bool IMG>
 __global__ void __launch_bounds__(SB2)
     k_screen_b2(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
                 B2View v, int32_t *__restrict__ lab_out, int64_t base,
-                int delta, int hint) {
+                int delta, int hint, XImage img) {
   typedef float f32x16 __attribute__((ext_vector_type(16)));
   constexpr int GB = 1 << (PACK2 - 4);  // 32-centre blocks per top-3 group
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -108,18 +119,28 @@ __global__ void __launch_bounds__(SB2)
   // W1: one own-mask word per column (k <= 1024), held in a register
   const int nkw = W1 ? 1 : (nkb + 31) >> 5;
   char *frag = (char *)smem;                                // nkb x NKS KB
-  float *cn = (float *)(frag + (int64_t)nkb * NKS * 1024);  // b1 order
-  float *ncn = cn + nkb * 32;                               // -|c|^2, plain
+  // b1-order norms for the top-3 fallback (PC: read from ncn instead)
+  float *cn = (float *)(frag + (int64_t)nkb * NKS * 1024);
+  float *ncn = cn + (PC ? 0 : nkb * 32);                    // -|c|^2, plain
   char *scr0 = (char *)(ncn + nkb * 32);
+  // PC: the ring, its flags, then the consumers' scratch
+  char *ring = scr0;
+  int *rflag = (int *)(ring + B2_S * b2_slot_bytes(NKS));  // full, freed, next
+  if (PC) scr0 = (char *)(rflag + 4 * B2_S);
   {
     const f32x4 *src = (const f32x4 *)v.b1frag;
     f32x4 *dst = (f32x4 *)frag;
     for (int e = threadIdx.x; e < nkb * NKS * 64; e += SB2) dst[e] = src[e];
     for (int e = threadIdx.x; e < nkb * 32; e += SB2) {
-      cn[e] = v.cn32f[e];
+      if (!PC) cn[e] = v.cn32f[e];
       // padding centres: -2^100 (never passes a sane threshold)
       ncn[e] = e < k ? -v.cn32[e] : -0x1.0p100f;
     }
+    if (PC && threadIdx.x < B2_S) {
+      rflag[threadIdx.x] = -1;                      // full: tile held
+      rflag[B2_S + threadIdx.x] = threadIdx.x - B2_S;  // freed: last read
+    }
+    if (PC && threadIdx.x == 0) rflag[2 * B2_S] = 0;  // next tile to claim
   }
   const float cm =
       (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
@@ -139,16 +160,25 @@ __global__ void __launch_bounds__(SB2)
 
   const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t wv = (int64_t)blockIdx.x * (SB2 / 64) + wid;
+  constexpr int NW = PC ? SB2 / 64 - B2_NLOAD : SB2 / 64;  // screening waves
+  const int cw = PC ? wid - B2_NLOAD : wid;  // screening wave index
+  const int64_t wv = (int64_t)blockIdx.x * NW + cw;
   const int64_t step = (int64_t)gridDim.x * (SB2 / 64) * 32;
-  char *scr = scr0 + (int64_t)wid * (B2_SCR_FIXED + 128 * nkw);
+  // PC: this workgroup's tiles are blockIdx.x + j gridDim.x, j < J
+  const int64_t ntiles = (n - base + 31) / 32;
+  const int64_t J = ntiles > blockIdx.x
+                        ? (ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x
+                        : 0;
+  char *scr = scr0 + (int64_t)(PC ? cw : wid) *
+                         ((PC ? B2_CSCR : B2_SCR_FIXED) + 128 * nkw);
   float *s_tn = (float *)scr;              // -T per sample
   int *s_hp = (int *)(scr + 128);          // hint per sample (-1: none)
   int *s_cnt = (int *)(scr + 256);         // kept entries appended
   float *s_xx = (float *)(scr + 384);      // |x|^2 per sample
   char *s_tx = scr + 512;                   // one K-step of the tile, bf16
   int2 *s_ent = (int2 *)(scr + 512);       // (score bits, centre), later
-  uint32_t *s_om = (uint32_t *)(scr + B2_SCR_FIXED);  // [word][column]
+  uint32_t *s_om =
+      (uint32_t *)(scr + (PC ? B2_CSCR : B2_SCR_FIXED));  // [word][column]
   int2 *wl = v.tlist + wv * TL_CAP;  // >= 3 candidates
   int2 *cl = v.clist + wv * B1_CAP;  // 2 candidates
   int4 *nl = v.nlist + wv * B1_NCAP; // 3..6 candidates
@@ -183,7 +213,7 @@ __global__ void __launch_bounds__(SB2)
   for (int i = 0; i < IC; ++i)
     lane_off[i] = (uint32_t)((RI * i + lrow) * ldx * (int64_t)sizeof(TX)) +
                   (uint32_t)(16 * lpos);
-  auto load_tile = [&](int64_t s0) {
+  auto load_into = [&](int64_t s0, tx4 (&dst)[NKS][IC], int &pvd) {
     const int64_t rows = std::max<int64_t>(0, n - s0);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(X + std::min(s0, n) * ldx), 0,
@@ -193,7 +223,7 @@ __global__ void __launch_bounds__(SB2)
       const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
           (void *)(lab_out + std::min(s0, n)), 0,
           (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
-      pv = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
+      pvd = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
     }
     // every load issued before the first use; rows past n read 0
     // (num_records), features past d are zeroed at conversion
@@ -201,71 +231,38 @@ __global__ void __launch_bounds__(SB2)
     for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
       for (int i = 0; i < IC; ++i)
-        raw[ks][i] = __builtin_bit_cast(
+        dst[ks][i] = __builtin_bit_cast(
             tx4, __builtin_amdgcn_raw_buffer_load_b128(
                      rx, lane_off[i] + 16 * ks * (int)sizeof(TX), 0, 0));
   };
+  auto load_tile = [&](int64_t s0) { load_into(s0, raw, pv); };
   // operand half of row `row` in the transpose: swizzled by (row >> 3) & 1
   // so that the ds_read_b128 lane groups hit 64 distinct banks
   auto tx_addr = [](int row, int half) {
     return 32 * row + 16 * (half ^ ((row >> 3) & 1));
   };
+  // a loading lane's piece of row RI i + lrow: tx_addr(row, half) + within
+  // = RI 32 i + wofs[i & 1] (fp64: (row >> 3) & 1 = i & 1; fp32: RI = 16,
+  // (row >> 3) & 1 = (lrow >> 3) & 1), two per-lane VGPRs and immediates
+  uint32_t wofs[2];
+  {
+    const int half = EPL == 2 ? lpos >> 2 : lpos >> 1;
+    const int within = EPL == 2 ? 4 * (lpos & 3) : 8 * (lpos & 1);
+#pragma unroll
+    for (int par = 0; par < 2; ++par)
+      wofs[par] = (uint32_t)(tx_addr(RI * par + lrow, half) - 32 * RI * par +
+                             within);
+  }
+  auto wofs_at = [&](int i) { return 32 * RI * i + wofs[EPL == 2 ? i & 1 : 0]; };
 
   // A/B (-DDKM_AB_B2_PF=1, pair with -DDKM_AB_SB2=512): the next tile's
   // loads are issued as soon as this one is converted
 #ifndef DKM_AB_B2_PF
 #define DKM_AB_B2_PF 0
 #endif
-  if (DKM_AB_B2_PF && base + wv * 32 < n) load_tile(base + wv * 32);
-  for (int64_t s0 = base + wv * 32; s0 < n; s0 += step) {
-    if (!DKM_AB_B2_PF) load_tile(s0);
-    bf16x8 xh[NKS];
-    float xp[IC];  // |x|^2 partials of rows RI i + lrow
-#pragma unroll
-    for (int i = 0; i < IC; ++i) xp[i] = 0.f;
-    // features past d (d % 16 != 0): lim recomputed per tile (opaque), or
-    // the lane masks are hoisted into long-lived SGPR pairs
-    const int lim = d == 16 * NKS ? 0x7fffffff
-                                  : (int)opaque_u32((uint32_t)(d - EPL * lpos));
-    wave_sync();  // the previous tile's kept entries were read
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-#pragma unroll
-      for (int i = 0; i < IC; ++i) {
-        float xf[EPL];
-#pragma unroll
-        for (int e = 0; e < EPL; ++e) {
-          const float x = (float)raw[ks][i][e];
-          xf[e] = 16 * ks + e < lim ? x : 0.f;
-          xp[i] = fmaf(xf[e], xf[e], xp[i]);
-        }
-        const int row = RI * i + lrow;
-        if constexpr (EPL == 2) {
-          const bf16x2 b2 = __builtin_convertvector(f32x2{xf[0], xf[1]}, bf16x2);
-          *(bf16x2 *)(s_tx + tx_addr(row, lpos >> 2) + 4 * (lpos & 3)) = b2;
-        } else {
-          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-          const bf16x2 a2 = __builtin_convertvector(f32x2{xf[0], xf[1]}, bf16x2);
-          const bf16x2 b2 = __builtin_convertvector(f32x2{xf[2], xf[3]}, bf16x2);
-          *(bf16x4 *)(s_tx + tx_addr(row, lpos >> 1) + 8 * (lpos & 1)) =
-              bf16x4{a2[0], a2[1], b2[0], b2[1]};
-        }
-      }
-      wave_sync();
-      xh[ks] = *(const bf16x8 *)(s_tx + tx_addr(r, h));
-      wave_sync();
-    }
-    // |x|^2: the LR lanes of a row line hold its partials
-#pragma unroll
-    for (int i = 0; i < IC; ++i) {
-#pragma unroll
-      for (int m = 1; m < LR; m <<= 1) xp[i] += __shfl_xor(xp[i], m, 64);
-      if (lpos == 0) s_xx[RI * i + lrow] = xp[i];
-    }
-    wave_sync();
-    const float xx = s_xx[r];
-    const int prv = pv;
-    if (DKM_AB_B2_PF && s0 + step < n) load_tile(s0 + step);
+  // ---- one tile: threshold pass (or top-3), decision, lists, labels ----
+  auto process = [&](int64_t s0, const bf16x8 (&xh)[NKS], float xx,
+                     int prv) {
     const int64_t si = s0 + r;
     float xn;
     const float B2 = bound2_fast(bk, xx, xn);
@@ -539,10 +536,19 @@ __global__ void __launch_bounds__(SB2)
     if (need3) {
       // ---- top-3 pass (no usable hint): b1's layout, centres on the rows --
       auto chain = [&](int cb, f32x16 &accv) {
-        const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
-        const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
-        accv = f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
-                      c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+        if constexpr (PC) {
+          // register g = centre cb*32 + (g & 3) + 8 (g >> 2) + 4h: four
+          // runs of 4 in the plain -|c|^2 table
+          const f32x4 *c4p = (const f32x4 *)(ncn + cb * 32 + 4 * h);
+          const f32x4 c0 = c4p[0], c1 = c4p[2], c2 = c4p[4], c3 = c4p[6];
+          accv = -f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                         c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+        } else {
+          const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
+          const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
+          accv = f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                        c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+        }
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
           const bf16x8 ah =
@@ -673,7 +679,198 @@ __global__ void __launch_bounds__(SB2)
     // that overflowed a list keeps -(prev + 2): the label scan finds it.
     if (valid && !nlisted && !(unique && i1 == (hint ? prv : prev)))
       lab_out[si] = unique ? i1 : -(prev + 2);
+  };
+
+  if constexpr (PC) {
+    // ---- producer/consumer: loaders stream tiles into the ring ----------
+    int *full = rflag, *freed = rflag + B2_S, *next = rflag + 2 * B2_S;
+    auto tile_s0 = [&](int64_t j) {
+      return base + ((int64_t)blockIdx.x + j * gridDim.x) * 32;
+    };
+    // bounded spin on an LDS word (a correct ring never reaches the bound;
+    // past it the wave stops waiting -- wrong labels, never a hung GPU)
+    auto wait_eq = [&](int *p, int want) {
+      for (int it = 0; it < (1 << 22); ++it) {
+        if (__hip_atomic_load(p, __ATOMIC_ACQUIRE,
+                              __HIP_MEMORY_SCOPE_WORKGROUP) == want)
+          return;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    };
+    if (wid < B2_NLOAD) {
+      // loader: its tiles j = wid, wid + NLOAD, ... with the next one's
+      // loads in flight while this one is converted into its slot
+      tx4 rawb[NKS][IC];
+      int pvb = -1;
+      auto publish = [&](int64_t j, const tx4 (&rw)[NKS][IC], int hp) {
+        const int sl = (int)(j % B2_S);
+        char *slot = ring + sl * b2_slot_bytes(NKS);
+        float *sxx = (float *)(slot + NKS * 1024);
+        int *shp = (int *)(slot + NKS * 1024 + 128);
+        wait_eq(&freed[sl], (int)j - B2_S);  // the slot's previous tile read
+        float xp[IC];
+#pragma unroll
+        for (int i = 0; i < IC; ++i) xp[i] = 0.f;
+        const int lim = d == 16 * NKS
+                            ? 0x7fffffff
+                            : (int)opaque_u32((uint32_t)(d - EPL * lpos));
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          char *stx = slot + ks * 1024;
+#pragma unroll
+          for (int i = 0; i < IC; ++i) {
+            float xf[EPL];
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) {
+              const float x = (float)rw[ks][i][e];
+              xf[e] = 16 * ks + e < lim ? x : 0.f;
+              xp[i] = fmaf(xf[e], xf[e], xp[i]);
+            }
+            if constexpr (EPL == 2) {
+              *(bf16x2 *)(stx + wofs_at(i)) =
+                  __builtin_convertvector(f32x2{xf[0], xf[1]}, bf16x2);
+            } else {
+              typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+              const bf16x2 a2 =
+                  __builtin_convertvector(f32x2{xf[0], xf[1]}, bf16x2);
+              const bf16x2 b2 =
+                  __builtin_convertvector(f32x2{xf[2], xf[3]}, bf16x2);
+              *(bf16x4 *)(stx + wofs_at(i)) = bf16x4{a2[0], a2[1], b2[0], b2[1]};
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < IC; ++i) {
+#pragma unroll
+          for (int m = 1; m < LR; m <<= 1) xp[i] += __shfl_xor(xp[i], m, 64);
+          if (lpos == 0) sxx[RI * i + lrow] = xp[i];
+        }
+        if (h == 0) shp[r] = hp;
+        // release: the slot's writes are complete before `full` says so
+        if (lane == 0)
+          __hip_atomic_store(&full[sl], (int)j, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      };
+      // two register sets, A = raw and B = rawb, alternating (unrolled:
+      // no runtime-indexed register arrays); publishing A waits only for
+      // A's loads, B's stay in flight
+      int64_t j = wid;
+      if (j < J) load_into(tile_s0(j), raw, pv);
+      for (; j < J; j += 2 * B2_NLOAD) {
+        if (j + B2_NLOAD < J) load_into(tile_s0(j + B2_NLOAD), rawb, pvb);
+        publish(j, raw, pv);
+        if (j + B2_NLOAD >= J) break;
+        if (j + 2 * B2_NLOAD < J) load_into(tile_s0(j + 2 * B2_NLOAD), raw, pv);
+        publish(j + B2_NLOAD, rawb, pvb);
+      }
+      return;
+    }
+    (void)img;
+    // consumer: claim tiles in order; read the slot into registers, free it
+    for (;;) {
+      int j = 0;
+      if (lane == 0) j = atomicAdd(next, 1);
+      j = __builtin_amdgcn_readfirstlane(j);
+      if (j >= J) break;
+      const int sl = j % B2_S;
+      const char *slot = ring + sl * b2_slot_bytes(NKS);
+      wait_eq(&full[sl], j);
+      bf16x8 xh[NKS];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+        xh[ks] = *(const bf16x8 *)(slot + ks * 1024 + tx_addr(r, h));
+      const float xx = ((const float *)(slot + NKS * 1024))[r];
+      const int prv = ((const int *)(slot + NKS * 1024 + 128))[r];
+      if (lane == 0)
+        __hip_atomic_store(&freed[sl], j, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      process(tile_s0(j), xh, xx, prv);
+    }
+  } else if constexpr (IMG) {
+    // ---- sample image: each lane's operand is one 16-B piece of a 1 KB
+    // K-step block (whole lines), |x|^2 precomputed; the next tile's
+    // loads are in flight while this one is screened
+    auto load_img = [&](int64_t s0, bf16x8 (&dst)[NKS], float &xxd, int &pvd) {
+      const bf16x8 *src =
+          (const bf16x8 *)(img.tiles + (s0 >> 5) * (NKS * 512)) + lane;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+        dst[ks] = __builtin_nontemporal_load(src + 64 * ks);
+      xxd = __builtin_nontemporal_load(img.xx + s0 + r);
+      if (delta || hint) {
+        const int64_t rows = std::max<int64_t>(0, n - s0);
+        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(lab_out + std::min(s0, n)), 0,
+            (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
+        pvd = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
+      }
+    };
+    int64_t s0 = base + wv * 32;
+    bf16x8 xq[NKS];
+    float xxq = 0.f;
+    int pq = -1;
+    if (s0 < n) load_img(s0, xq, xxq, pq);
+    for (; s0 < n; s0 += step) {
+      bf16x8 xh[NKS];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) xh[ks] = xq[ks];
+      const float xx = xxq;
+      const int prv = pq;
+      if (s0 + step < n) load_img(s0 + step, xq, xxq, pq);
+      process(s0, xh, xx, prv);
+    }
+  } else {
+  if (DKM_AB_B2_PF && base + wv * 32 < n) load_tile(base + wv * 32);
+  for (int64_t s0 = base + wv * 32; s0 < n; s0 += step) {
+    if (!DKM_AB_B2_PF) load_tile(s0);
+    bf16x8 xh[NKS];
+    float xp[IC];  // |x|^2 partials of rows RI i + lrow
+#pragma unroll
+    for (int i = 0; i < IC; ++i) xp[i] = 0.f;
+    // features past d (d % 16 != 0): lim recomputed per tile (opaque), or
+    // the lane masks are hoisted into long-lived SGPR pairs
+    const int lim = d == 16 * NKS ? 0x7fffffff
+                                  : (int)opaque_u32((uint32_t)(d - EPL * lpos));
+    wave_sync();  // the previous tile's kept entries were read
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+      for (int i = 0; i < IC; ++i) {
+        float xf[EPL];
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          const float x = (float)raw[ks][i][e];
+          xf[e] = 16 * ks + e < lim ? x : 0.f;
+          xp[i] = fmaf(xf[e], xf[e], xp[i]);
+        }
+        if constexpr (EPL == 2) {
+          const bf16x2 b2 = __builtin_convertvector(f32x2{xf[0], xf[1]}, bf16x2);
+          *(bf16x2 *)(s_tx + wofs_at(i)) = b2;
+        } else {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          const bf16x2 a2 = __builtin_convertvector(f32x2{xf[0], xf[1]}, bf16x2);
+          const bf16x2 b2 = __builtin_convertvector(f32x2{xf[2], xf[3]}, bf16x2);
+          *(bf16x4 *)(s_tx + wofs_at(i)) = bf16x4{a2[0], a2[1], b2[0], b2[1]};
+        }
+      }
+      wave_sync();
+      xh[ks] = *(const bf16x8 *)(s_tx + tx_addr(r, h));
+      wave_sync();
+    }
+    // |x|^2: the LR lanes of a row line hold its partials
+#pragma unroll
+    for (int i = 0; i < IC; ++i) {
+#pragma unroll
+      for (int m = 1; m < LR; m <<= 1) xp[i] += __shfl_xor(xp[i], m, 64);
+      if (lpos == 0) s_xx[RI * i + lrow] = xp[i];
+    }
+    wave_sync();
+    const float xx = s_xx[r];
+    const int prv = pv;
+    if (DKM_AB_B2_PF && s0 + step < n) load_tile(s0 + step);
+    process(s0, xh, xx, prv);
   }
+  }  // !PC
   if (lane == 0 && listing) {
     v.tcount[wv] = tl_cnt;
     v.ccount[wv] = cl_cnt;
@@ -694,6 +891,15 @@ size_t b2_lds_bytes(int64_t k, int64_t d) {
          (size_t)(SB2 / 64) * (B2_SCR_FIXED + 128 * nkw);
 }
 
+// the producer/consumer form's LDS image (no b1-order norm copy)
+static size_t b2pc_lds_bytes(int64_t k, int64_t d) {
+  const int64_t nkb = kpad32(k) / 32, nkw = (nkb + 31) / 32;
+  const int nks = (int)(dpad16(d) / 16);
+  return (size_t)nkb * nks * 1024 + (size_t)nkb * 128 +
+         (size_t)B2_S * b2_slot_bytes(nks) + 16 * B2_S +
+         (size_t)(SB2 / 64 - B2_NLOAD) * (B2_CSCR + 128 * nkw);
+}
+
 // DKM_B1_LEGACY=1 runs k_screen_b1 instead (A/B and its parity tests); read
 // per launch so that one process can run both
 int b2_probe() { return DKM_AB_B2_PROBE; }
@@ -703,20 +909,130 @@ bool b2_enabled() {
   return !(e && *e && *e != '0');
 }
 
+// DKM_B2_PC=1: the producer/consumer form (4 loader waves feeding 8
+// screening waves through an LDS ring).  Off by default: at C3 it ran
+// 39.8 ms per launch against 24.0 ms for every wave loading its own tiles
+// (profiles/r03/b2/r03g_*): the loaders' two register tiles spill, and 8
+// screening waves hide less than 12.  Read per launch.
+static bool b2pc_enabled() {
+  const char *e = getenv("DKM_B2_PC");
+  return e && *e == '1';
+}
+
+// ---- the sample image (dkm_x_image_*) ----------------------------------
+size_t x_image_bytes(int64_t n, int64_t d) {
+  const int64_t nt = (n + 31) / 32;
+  return (size_t)nt * (dpad16(d) / 16) * 1024 + (size_t)nt * 128;
+}
+
+XImage x_image_view(const void *image, int64_t n, int64_t d) {
+  XImage im;
+  im.tiles = (const uint16_t *)image;
+  im.xx = (const float *)((const char *)image +
+                          (size_t)((n + 31) / 32) * (dpad16(d) / 16) * 1024);
+  return im;
+}
+
+// One workgroup per 32-row tile (grid-stride): the tile's rows are read
+// with consecutive lanes on consecutive features (whole lines), staged as
+// fp32 in LDS, then written in operand order -- lane l of K-step ks holds
+// row l & 31, features 16 ks + 8 (l >> 5) .. + 7 -- with the same
+// fp64 -> fp32 -> bf16 roundings the converting screen applies.  |x|^2 is
+// summed in fp64 over the fp32 values and rounded once.
+template <class TX, int NKS>
+__global__ void __launch_bounds__(256)
+    k_x_image(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
+              uint16_t *__restrict__ tiles, float *__restrict__ xx) {
+  constexpr int DP = 16 * NKS, LD = DP + 4;
+  __shared__ float s[32 * LD];
+  const int64_t nt = (n + 31) / 32;
+  for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int64_t r0 = t * 32;
+    __syncthreads();  // the previous tile's reads are done
+    for (int e = threadIdx.x; e < 32 * DP; e += 256) {
+      const int row = e / DP, col = e % DP;
+      float v = 0.f;
+      if (r0 + row < n && col < d) v = (float)X[(r0 + row) * ldx + col];
+      s[row * LD + col] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      double a = 0.0;
+      for (int c = 0; c < DP; ++c) {
+        const double v = s[threadIdx.x * LD + c];
+        a = fma(v, v, a);
+      }
+      xx[r0 + threadIdx.x] = (float)a;
+    }
+    for (int e = threadIdx.x; e < NKS * 64; e += 256) {
+      const int ks = e >> 6, l = e & 63;
+      const float *src = s + (l & 31) * LD + 16 * ks + 8 * (l >> 5);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const bf16x2 b = __builtin_convertvector(f32x2{src[j], src[j + 1]},
+                                                 bf16x2);
+        o[j] = b[0];
+        o[j + 1] = b[1];
+      }
+      *((bf16x8 *)(tiles + t * (NKS * 512)) + e) = o;
+    }
+  }
+}
+
+template <class TX>
+int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, void *image,
+                   int cus, hipStream_t s) {
+  const int nks = (int)(dpad16(d) / 16);
+  const XImage im = x_image_view(image, n, d);
+  const int64_t nt = (n + 31) / 32;
+  const unsigned g =
+      (unsigned)std::max<int64_t>(1, std::min<int64_t>(nt, (int64_t)cus * 8));
+  uint16_t *tiles = (uint16_t *)image;
+  float *xx = (float *)im.xx;
+  switch (nks) {
+#define DKM_XI(N)                                                         \
+  case N:                                                                 \
+    k_x_image<TX, N><<<g, 256, 0, s>>>(X, n, d, ldx, tiles, xx);          \
+    break;
+    DKM_XI(1) DKM_XI(2) DKM_XI(3) DKM_XI(4)
+    DKM_XI(5) DKM_XI(6) DKM_XI(7) DKM_XI(8)
+#undef DKM_XI
+    default:
+      return fail(DKM_E_ARG, "x_image: d > 128");
+  }
+  return check_launch("sample image");
+}
+
+template int launch_x_image<double>(const double *, int64_t, int, int64_t,
+                                    void *, int, hipStream_t);
+template int launch_x_image<float>(const float *, int64_t, int, int64_t,
+                                   void *, int, hipStream_t);
+
 template <class TX>
 int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
                      const WsView &v, int32_t *lab_out, int64_t base, int hint,
-                     int cus, hipStream_t s, int *nseg) {
-  const size_t lds = b2_lds_bytes(k, d);
+                     int cus, hipStream_t s, int *nseg, XImage img) {
+  const bool pc = b2pc_enabled() && SB2 / 64 > B2_NLOAD &&
+                  b2pc_lds_bytes(k, d) <= 160 * 1024;
+  const size_t lds = pc ? b2pc_lds_bytes(k, d) : b2_lds_bytes(k, d);
   if (lds > 160 * 1024) return 1;  // caller uses k_screen_b1
+  // the image path reads whole tiles: the range must start on one
+  const bool im = img.tiles && !pc && base % 32 == 0;
+  if (!im) img = XImage{nullptr, nullptr};
   const int nks = (int)(dpad16(d) / 16);
   const bool w1 = kpad32(k) <= 1024;
   const void *kf = nullptr;
+#define DKM_B2K(N, W, P, I) (const void *)k_screen_b2<TX, N, W, P, I>
   switch (nks) {
-#define DKM_B2(N)                                                  \
-  case N:                                                          \
-    kf = w1 ? (const void *)k_screen_b2<TX, N, true>               \
-            : (const void *)k_screen_b2<TX, N, false>;             \
+#define DKM_B2(N)                                                          \
+  case N:                                                                  \
+    kf = pc ? (w1 ? DKM_B2K(N, true, true, false)                          \
+                  : DKM_B2K(N, false, true, false))                        \
+       : im ? (w1 ? DKM_B2K(N, true, false, true)                          \
+                  : DKM_B2K(N, false, false, true))                        \
+            : (w1 ? DKM_B2K(N, true, false, false)                         \
+                  : DKM_B2K(N, false, false, false));                      \
     break;
     DKM_B2(1) DKM_B2(2) DKM_B2(3) DKM_B2(4)
     DKM_B2(5) DKM_B2(6) DKM_B2(7) DKM_B2(8)
@@ -727,11 +1043,12 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
   if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return fail(DKM_E_LAUNCH, "screen_b2: LDS attribute");
-  const int64_t need = (end - base + 32 * (SB2 / 64) - 1) / (32 * (SB2 / 64));
+  const int nw = pc ? SB2 / 64 - B2_NLOAD : SB2 / 64;  // screening waves
+  const int64_t need = pc ? (end - base + 31) / 32
+                          : (end - base + 32 * nw - 1) / (32 * nw);
   const unsigned g =
       (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)cus));
-  *nseg = (int)std::min<int64_t>((int64_t)g * (SB2 / 64),
-                                 std::min(TL_SEGS, B1_SEGS));
+  *nseg = (int)std::min<int64_t>((int64_t)g * nw, std::min(TL_SEGS, B1_SEGS));
   const int delta = 0;  // labels only (the sums come from the labels)
   B2View bv;
   bv.hdr = v.hdr;
@@ -744,28 +1061,19 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
   bv.tcount = v.tcount;
   bv.ccount = v.ccount;
   bv.ncount = v.ncount;
-  switch (nks) {
-#define DKM_B2L(N)                                                      \
-  case N:                                                               \
-    if (w1)                                                             \
-      k_screen_b2<TX, N, true><<<g, SB2, lds, s>>>(                     \
-          X, end, d, ldx, k, bv, lab_out, base, delta, hint);           \
-    else                                                                \
-      k_screen_b2<TX, N, false><<<g, SB2, lds, s>>>(                    \
-          X, end, d, ldx, k, bv, lab_out, base, delta, hint);           \
-    break;
-    DKM_B2L(1) DKM_B2L(2) DKM_B2L(3) DKM_B2L(4)
-    DKM_B2L(5) DKM_B2L(6) DKM_B2L(7) DKM_B2L(8)
-#undef DKM_B2L
-  }
+  hipLaunchKernelGGL((void (*)(const TX *, int64_t, int, int64_t, int, B2View,
+                               int32_t *, int64_t, int, int, XImage))kf,
+                     dim3(g), dim3(SB2), lds, s, X, end, d, ldx, k, bv,
+                     lab_out, base, delta, hint, img);
+#undef DKM_B2K
   return check_launch("screen assignment (single product, centres on lanes)");
 }
 
 template int launch_screen_b2<double>(const double *, int64_t, int, int64_t,
                                       int, const WsView &, int32_t *, int64_t,
-                                      int, int, hipStream_t, int *);
+                                      int, int, hipStream_t, int *, XImage);
 template int launch_screen_b2<float>(const float *, int64_t, int, int64_t, int,
                                      const WsView &, int32_t *, int64_t, int,
-                                     int, hipStream_t, int *);
+                                     int, hipStream_t, int *, XImage);
 
 }  // namespace dkm

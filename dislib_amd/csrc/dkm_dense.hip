@@ -2693,7 +2693,7 @@ template <class TX>
 static int launch_screen(int prec, const TX *X, int64_t n, int d,
                          int64_t ldx, const double *C, int k, const WsView &v,
                          size_t wsb, int32_t *labels, double *acc,
-                         int acc_kind, hipStream_t s) {
+                         int acc_kind, hipStream_t s, XImage img) {
   (void)wsb;
   const int64_t nq = std::min<int64_t>(v.nq, INT32_MAX);
   if (!labels && nq < 1)
@@ -2747,7 +2747,7 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
       const int hint = labels && acc_kind != 0 ? 1 : 0;
       r = b2_enabled() ? launch_screen_b2<TX>(X, end, d, ldx, k, v, lab_out,
                                               base, hint, dev_info().cus, s,
-                                              &nseg)
+                                              &nseg, img)
                        : 1;
       if (r == 1)
         r = launch_screen_b1<TX>(X, end, d, ldx, k, v, lab_out, base, hint, s,
@@ -2830,7 +2830,7 @@ template <class TX>
 static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                   const double *C, int64_t k, const void *ws, size_t wsb,
                   int32_t *labels, double *acc, int acc_kind, int mode,
-                  void *stream, const char *who) {
+                  void *stream, const char *who, const void *image = nullptr) {
   if (n < 0 || d <= 0 || k <= 0 || ldx < d)
     return fail(DKM_E_ARG, std::string(who) + ": bad n/d/k/ldx");
   if (d > INT32_MAX || k > INT32_MAX)
@@ -2868,10 +2868,27 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
     const int prec = mode == DKM_MODE_SCREEN32 ? P_F32
                      : mode == DKM_MODE_SCREEN_BF16 ? P_B1
                                                     : P_B3;
+    const XImage img = image ? x_image_view(image, n, d)
+                             : XImage{nullptr, nullptr};
     return launch_screen<TX>(prec, X, n, (int)d, ldx, C, (int)k, v, wsb,
-                             labels, acc, acc_kind, s);
+                             labels, acc, acc_kind, s, img);
   }
   return fail(DKM_E_ARG, std::string(who) + ": bad mode");
+}
+
+template <class TX>
+static int x_image(const TX *X, int64_t n, int64_t d, int64_t ldx,
+                   void *image, size_t image_bytes, void *stream,
+                   const char *who) {
+  if (n < 0 || d <= 0 || ldx < d)
+    return fail(DKM_E_ARG, std::string(who) + ": bad n/d/ldx");
+  if (d > 128) return fail(DKM_E_ARG, std::string(who) + ": d > 128");
+  if (n == 0) return 0;
+  if (!X || !image) return fail(DKM_E_ARG, std::string(who) + ": NULL");
+  if (image_bytes < x_image_bytes(n, d))
+    return fail(DKM_E_WORKSPACE, std::string(who) + ": image too small");
+  return launch_x_image<TX>(X, n, (int)d, ldx, image, dev_info().cus,
+                            (hipStream_t)stream);
 }
 
 }  // namespace dkm
@@ -2932,6 +2949,73 @@ int dkm_predict_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
   if (!labels) return fail(DKM_E_ARG, "predict: labels is NULL");
   return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, nullptr, 0,
                        mode, stream, "dkm_predict_f32");
+}
+
+int dkm_x_image_useful(int64_t k, int64_t d, int mode) {
+  if (k <= 0 || d <= 0 || d > 128 || k > INT32_MAX) return 0;
+  if (gemm_path(k, d) || !screen_ok(k, d) || !b1_ok(k, d)) return 0;
+  const bool single = mode == DKM_MODE_SCREEN_BF16 ||
+                      (mode == DKM_MODE_AUTO && !sums_fit_lds(k, d));
+  return single && b2_enabled() && b2_lds_bytes(k, d) <= 160 * 1024 ? 1 : 0;
+}
+
+size_t dkm_x_image_bytes(int64_t n, int64_t d) {
+  if (n < 0 || d <= 0 || d > 128) return 0;
+  return x_image_bytes(n, d);
+}
+
+int dkm_x_image_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
+                    void *image, size_t image_bytes, void *stream) {
+  return x_image<double>(X, n, d, ldx, image, image_bytes, stream,
+                         "dkm_x_image_f64");
+}
+
+int dkm_x_image_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
+                    void *image, size_t image_bytes, void *stream) {
+  return x_image<float>(X, n, d, ldx, image, image_bytes, stream,
+                        "dkm_x_image_f32");
+}
+
+int dkm_partial_sum_img_f64(const double *X, const void *image, int64_t n,
+                            int64_t d, int64_t ldx, const double *C,
+                            int64_t k, const void *ws, size_t ws_bytes,
+                            int32_t *labels, double *acc, int mode,
+                            void *stream) {
+  if (!acc) return fail(DKM_E_ARG, "partial_sum: acc is NULL");
+  return assign<double>(X, n, d, ldx, C, k, ws, ws_bytes, labels, acc, 1,
+                        mode, stream, "dkm_partial_sum_img_f64", image);
+}
+
+int dkm_partial_sum_img_f32(const float *X, const void *image, int64_t n,
+                            int64_t d, int64_t ldx, const double *C,
+                            int64_t k, const void *ws, size_t ws_bytes,
+                            int32_t *labels, double *acc, int mode,
+                            void *stream) {
+  if (!acc) return fail(DKM_E_ARG, "partial_sum: acc is NULL");
+  return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, acc, 1,
+                       mode, stream, "dkm_partial_sum_img_f32", image);
+}
+
+int dkm_assign_delta_img_f64(const double *X, const void *image, int64_t n,
+                             int64_t d, int64_t ldx, const double *C,
+                             int64_t k, const void *ws, size_t ws_bytes,
+                             int32_t *labels, double *delta, int mode,
+                             void *stream) {
+  if (!labels || !delta)
+    return fail(DKM_E_ARG, "assign_delta: labels and delta are required");
+  return assign<double>(X, n, d, ldx, C, k, ws, ws_bytes, labels, delta, 2,
+                        mode, stream, "dkm_assign_delta_img_f64", image);
+}
+
+int dkm_assign_delta_img_f32(const float *X, const void *image, int64_t n,
+                             int64_t d, int64_t ldx, const double *C,
+                             int64_t k, const void *ws, size_t ws_bytes,
+                             int32_t *labels, double *delta, int mode,
+                             void *stream) {
+  if (!labels || !delta)
+    return fail(DKM_E_ARG, "assign_delta: labels and delta are required");
+  return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, delta, 2,
+                       mode, stream, "dkm_assign_delta_img_f32", image);
 }
 
 int dkm_add_f64(double *y, const double *x, int64_t n, void *stream) {

@@ -768,6 +768,31 @@ int gemm_prepare(const double *C, int64_t k, int64_t d, const WsView &v,
   return check_launch("gemm_prepare");
 }
 
+// the second stream of gemm_screen and its events, one set per device and
+// host thread (created at first use, kept for the process)
+struct SplitStream {
+  hipStream_t s = nullptr;
+  hipEvent_t split_ev[2] = {nullptr, nullptr}, free_ev[2] = {nullptr, nullptr};
+  bool ok = false;
+};
+static SplitStream &split_stream() {
+  static thread_local SplitStream st[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  SplitStream &x = st[dev];
+  if (!x.ok) {
+    bool good =
+        hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) == hipSuccess;
+    for (int i = 0; i < 2 && good; ++i)
+      good = hipEventCreateWithFlags(&x.split_ev[i],
+                                     hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&x.free_ev[i],
+                                     hipEventDisableTiming) == hipSuccess;
+    x.ok = good;
+  }
+  return x;
+}
+
 template <class TX>
 int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
                 const double *C, int k, const WsView &v, int32_t *lab_out,
@@ -784,40 +809,72 @@ int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
   const int dpad = one ? (int)dpad64(d) : (int)dpad32(d);
   // bit 2: the single-product bound in the merge and candidate steps
   const int flags = (acc ? 1 : 0) | (delta ? 2 : 0) | (one ? 4 : 0);
-  for (int64_t c0 = base; c0 < end; c0 += v.gchunk) {
+  // The split of chunk c + 1 (HBM-bound) runs on a second stream while
+  // chunk c is screened (MFMA-bound): split buffers alternate, chunk c's
+  // screen waits for its split, and split c + 2 waits until chunk c's
+  // screen, merge and candidates (the readers of its buffer) are done.
+  SplitStream &ss = split_stream();
+  if (!ss.ok) return fail(DKM_E_LAUNCH, "gemm: second stream");
+  char *xs_b[2] = {v.gxs, v.gxs1};
+  float *xn_b[2] = {v.gxn, v.gxn1};
+  // the split reads X: after everything already queued on the caller's
+  // stream; both buffers start free
+  if (hipEventRecord(ss.free_ev[0], s) != hipSuccess ||
+      hipEventRecord(ss.free_ev[1], s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "gemm: event");
+  auto split = [&](int64_t c0, int b) -> int {
+    const int64_t rows = std::min<int64_t>(v.gchunk, end - c0);
+    if (hipStreamWaitEvent(ss.s, ss.free_ev[b], 0) != hipSuccess)
+      return fail(DKM_E_LAUNCH, "gemm: stream wait");
+    if (int r = launch_split<TX>(X, c0, rows, round_up(rows, GT), d, ldx, 1.0,
+                                 xs_b[b], xn_b[b], one ? 1 : 0, ss.s))
+      return r;
+    if (hipEventRecord(ss.split_ev[b], ss.s) != hipSuccess)
+      return fail(DKM_E_LAUNCH, "gemm: event");
+    return 0;
+  };
+  if (base < end)
+    if (int r = split(base, 0)) return r;
+  int b = 0;
+  for (int64_t c0 = base; c0 < end; c0 += v.gchunk, b ^= 1) {
     const int64_t rows = std::min<int64_t>(v.gchunk, end - c0);
     const int64_t mrows = round_up(rows, GT);
     const int nst = (int)(mrows / GT);
-    if (int r = launch_split<TX>(X, c0, rows, mrows, d, ldx, 1.0, v.gxs,
-                                 v.gxn, one ? 1 : 0, s))
-      return r;
+    if (c0 + v.gchunk < end)
+      if (int r = split(c0 + v.gchunk, b ^ 1)) return r;
+    if (hipStreamWaitEvent(s, ss.split_ev[b], 0) != hipSuccess)
+      return fail(DKM_E_LAUNCH, "gemm: stream wait");
+    WsView vb = v;  // the merge and candidate steps read this chunk's xn
+    vb.gxn = xn_b[b];
     if (one)
       k_gemm_screen<1><<<(unsigned)(nst * nct), GTHREADS, GLDS, s>>>(
-          v.gfrag1, v.gcn, v.gxs, nst, nct, nks, v.gpart);
+          v.gfrag1, v.gcn, xs_b[b], nst, nct, nks, v.gpart);
     else
       k_gemm_screen<3><<<(unsigned)(nst * nct), GTHREADS, GLDS, s>>>(
-          v.gfrag, v.gcn, v.gxs, nst, nct, nks, v.gpart);
+          v.gfrag, v.gcn, xs_b[b], nst, nct, nks, v.gpart);
     if (int r = check_launch("gemm screen")) return r;
     // both list counters (gcount, gcount2: adjacent words)
     if (hipMemsetAsync(&v.hdr->gcount, 0, 8, s) != hipSuccess)
       return fail(DKM_E_LAUNCH, "gemm: list reset");
     const unsigned mb = (unsigned)std::min<int64_t>((rows + 255) / 256, 8192);
     k_gemm_merge<TX><<<mb, 256, 0, s>>>(X, c0, rows, d, ldx, k, nct, dpad,
-                                        v.gpart, v.gxn, v, lab_out, acc,
+                                        v.gpart, xn_b[b], vb, lab_out, acc,
                                         flags);
     if (int r = check_launch("gemm merge")) return r;
     // a wave per listed sample: rows / 64 waves cover any list length
     const unsigned cb = (unsigned)((rows + 255) / 256);
     if (d <= 8192)
       k_gemm_cand<true, TX><<<cb, 256, 0, s>>>(X, c0, d, ldx, C, k, nct, dpad,
-                                               v.gpart, v.gxn, v, lab_out,
+                                               v.gpart, xn_b[b], vb, lab_out,
                                                acc, flags);
     else
       k_gemm_cand<false, TX><<<cb, 256, 0, s>>>(X, c0, d, ldx, C, k, nct,
-                                                dpad, v.gpart, v.gxn, v,
+                                                dpad, v.gpart, xn_b[b], vb,
                                                 lab_out, acc, flags);
     if (int r = check_launch("gemm candidates")) return r;
-    k_gemm_full<TX><<<256, 1024, 0, s>>>(X, c0, d, ldx, k, v, lab_out, acc,
+    if (hipEventRecord(ss.free_ev[b], s) != hipSuccess)
+      return fail(DKM_E_LAUNCH, "gemm: event");
+    k_gemm_full<TX><<<256, 1024, 0, s>>>(X, c0, d, ldx, k, vb, lab_out, acc,
                                          flags);
     if (int r = check_launch("gemm full scan")) return r;
   }

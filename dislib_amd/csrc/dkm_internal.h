@@ -126,6 +126,8 @@ struct WsView {
   float *gcn;      // kpad256 fp32 ||c||^2, 2^100 for padding centres
   char *gxs;       // gemm_chunk samples: split tiles of the current chunk
   float *gxn;      // gemm_chunk fp32 upper bounds of ||x||
+  char *gxs1;      // the same for the next chunk (split while the current
+  float *gxn1;     // chunk is screened, on a second stream)
   int2 *gpart;     // gemm_chunk x kpad256/GT x GTOP (score bits, centre)
   int64_t gchunk;  // samples per split chunk
   // sorted sums (dkm_sums.hip; k <= SORT_KMAX, else NULL)
@@ -145,10 +147,24 @@ struct WsView {
 bool b2_enabled();
 int b2_probe();  // != 0: a result-invalidating timing probe build
 size_t b2_lds_bytes(int64_t k, int64_t d);
+// The sample image (dkm_x_image_*): X's rows as bf16 MFMA A operands,
+// 32-row tiles of dpad16(d) / 16 K-steps x 1 KB, then fp32 |x|^2 per row
+// (rows and features past n, d zero).  With one, k_screen_b2 streams
+// 2 B per feature instead of sizeof(TX) and skips the conversion.
+struct XImage {
+  const uint16_t *tiles;
+  const float *xx;
+};
+size_t x_image_bytes(int64_t n, int64_t d);
+XImage x_image_view(const void *image, int64_t n, int64_t d);
+template <class TX>
+int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, void *image,
+                   int cus, hipStream_t s);
 template <class TX>
 int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
                      const WsView &v, int32_t *lab_out, int64_t base,
-                     int hint, int cus, hipStream_t s, int *nseg);
+                     int hint, int cus, hipStream_t s, int *nseg,
+                     XImage img);
 
 // Sorted sums: counting sort of the sample indices by label (LDS histograms
 // of k bins: k <= SORT_KMAX), then segmented row sums.

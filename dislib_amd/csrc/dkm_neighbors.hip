@@ -27,8 +27,8 @@
 //                  counts (int64 atomics per lane-partition), pass 1 writes
 //                  (index, distance) at an atomically advanced cursor;
 //     k_seg_sort   block per query list: (distance, index) ascending --
-//                  bitonic in LDS up to 4096 entries, a rank sort through
-//                  workspace scratch beyond.
+//                  bitonic in LDS up to 4096 entries; beyond, sorted runs
+//                  of 4096 merged pairwise through workspace scratch.
 #include "dkm_internal.h"
 
 #include <algorithm>
@@ -56,12 +56,14 @@ struct TopK {
     }
   }
   // (v, j) with j larger than every index already held (scan order), so a
-  // strict < keeps the earlier index first among equal r
+  // strict < keeps the earlier index first among equal r; an empty slot
+  // (+inf, INT32_MAX) also takes a row at +inf (overflowed distance), so
+  // every list fills with real rows (sklearn returns them too)
   __device__ __forceinline__ void push_seq(double v, int j) {
-    if (v < r[K - 1]) {
+    if (v < r[K - 1] || (v == r[K - 1] && i[K - 1] == INT32_MAX)) {
 #pragma unroll
       for (int s = 0; s < K; ++s) {
-        const bool lt = v < r[s];
+        const bool lt = v < r[s] || (v == r[s] && i[s] == INT32_MAX);
         const double tr = r[s];
         const int ti = i[s];
         r[s] = lt ? v : tr;
@@ -283,20 +285,82 @@ __global__ void __launch_bounds__(NB)
     }
     return;
   }
-  // beyond LDS: rank of each entry among the list (keys are distinct: the
-  // indices are), written to the scratch copy, then copied back
-  for (int64_t e = threadIdx.x; e < m; e += NB) {
-    const double de = dist[o + e];
-    const int64_t ie = idx[o + e];
-    int64_t rank = 0;
-    for (int64_t f = 0; f < m; ++f) rank += key_lt(dist[o + f], idx[o + f], de, ie);
-    sdist[o + rank] = de;
-    sidx[o + rank] = ie;
+  // beyond LDS: sort runs of SORT_CAP in LDS (bitonic, written back in
+  // place), then merge run pairs through the scratch copy: an entry's
+  // place in the merged run = its place in its own run + the count of the
+  // other run's keys below it (binary search; keys are distinct since the
+  // indices are).  O(m log^2 m) per list instead of the rank sort's O(m^2)
+  // (a dense epsilon-ball of 1e5 neighbours was 1e10 comparisons).
+  for (int64_t c0 = 0; c0 < m; c0 += SORT_CAP) {
+    const int mc = (int)std::min<int64_t>(SORT_CAP, m - c0);
+    int p2 = 2;
+    while (p2 < mc) p2 <<= 1;
+    __syncthreads();
+    for (int e = threadIdx.x; e < p2; e += NB) {
+      sd[e] = e < mc ? dist[o + c0 + e] : INFINITY;
+      si[e] = e < mc ? idx[o + c0 + e] : INT64_MAX;
+    }
+    __syncthreads();
+    for (int size = 2; size <= p2; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int e = threadIdx.x; e < p2; e += NB) {
+          const int f = e ^ stride;
+          if (f > e) {
+            const bool up = (e & size) == 0;
+            const bool gt = key_lt(sd[f], si[f], sd[e], si[e]);
+            if (gt == up) {
+              const double td = sd[e];
+              sd[e] = sd[f];
+              sd[f] = td;
+              const int64_t ti = si[e];
+              si[e] = si[f];
+              si[f] = ti;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (int e = threadIdx.x; e < mc; e += NB) {
+      dist[o + c0 + e] = sd[e];
+      idx[o + c0 + e] = si[e];
+    }
   }
   __syncthreads();
-  for (int64_t e = threadIdx.x; e < m; e += NB) {
-    dist[o + e] = sdist[o + e];
-    idx[o + e] = sidx[o + e];
+  double *sdd = dist + o, *ddd = sdist + o;
+  int64_t *sii = idx + o, *dii = sidx + o;
+  for (int64_t run = SORT_CAP; run < m; run <<= 1) {
+    for (int64_t e = threadIdx.x; e < m; e += NB) {
+      const int64_t lo = e / (2 * run) * (2 * run);
+      const int64_t mid = std::min(lo + run, m), hi = std::min(lo + 2 * run, m);
+      const double de = sdd[e];
+      const int64_t ie = sii[e];
+      // the other run of the pair, and the count of its keys below (e)
+      const bool first = e < mid;
+      int64_t a = first ? mid : lo, b = first ? hi : mid;
+      while (a < b) {
+        const int64_t c = (a + b) >> 1;
+        if (key_lt(sdd[c], sii[c], de, ie))
+          a = c + 1;
+        else
+          b = c;
+      }
+      const int64_t pos = first ? e + (a - mid) : (e - mid) + lo + (a - lo);
+      ddd[pos] = de;
+      dii[pos] = ie;
+    }
+    __syncthreads();
+    double *td = sdd;
+    sdd = ddd;
+    ddd = td;
+    int64_t *ti = sii;
+    sii = dii;
+    dii = ti;
+  }
+  if (sdd != dist + o) {  // the sorted list ended in the scratch copy
+    for (int64_t e = threadIdx.x; e < m; e += NB) {
+      dist[o + e] = sdd[e];
+      idx[o + e] = sii[e];
+    }
   }
 }
 

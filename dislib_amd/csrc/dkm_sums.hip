@@ -117,18 +117,22 @@ __global__ void __launch_bounds__(SBLK)
                  int64_t nh, int64_t lo, int k, int32_t *__restrict__ cnt) {
   extern __shared__ int hist[];
   const int64_t n = n_items(ndev, nh);
-  const int64_t p0 = (int64_t)blockIdx.x * SRANGE;
-  if (p0 >= n) return;
-  const int64_t p1 = std::min(n, p0 + SRANGE);
-  for (int c = threadIdx.x; c < k; c += SBLK) hist[c] = 0;
-  __syncthreads();
-  for (int64_t p = p0 + threadIdx.x; p < p1; p += SBLK) {
-    const int c = key[item_at(items, lo, p)];
-    if ((unsigned)c < (unsigned)k) atomicAdd(&hist[c], 1);
+  // block-stride over SRANGE chunks: an explicit list (delta path) is
+  // launched on a fixed grid and is usually short or empty
+  for (int64_t p0 = (int64_t)blockIdx.x * SRANGE; p0 < n;
+       p0 += (int64_t)gridDim.x * SRANGE) {
+    const int64_t p1 = std::min(n, p0 + SRANGE);
+    __syncthreads();
+    for (int c = threadIdx.x; c < k; c += SBLK) hist[c] = 0;
+    __syncthreads();
+    for (int64_t p = p0 + threadIdx.x; p < p1; p += SBLK) {
+      const int c = key[item_at(items, lo, p)];
+      if ((unsigned)c < (unsigned)k) atomicAdd(&hist[c], 1);
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < k; c += SBLK)
+      if (hist[c]) atomicAdd(&cnt[c], hist[c]);
   }
-  __syncthreads();
-  for (int c = threadIdx.x; c < k; c += SBLK)
-    if (hist[c]) atomicAdd(&cnt[c], hist[c]);
 }
 
 // Exclusive scan of cnt[0..k) -> off[0..k], cur = off (one block).
@@ -166,26 +170,28 @@ __global__ void __launch_bounds__(SBLK)
   extern __shared__ int hist[];  // [k] counts, then ranks; [k] bases
   int *base = hist + k;
   const int64_t n = n_items(ndev, nh);
-  const int64_t p0 = (int64_t)blockIdx.x * SRANGE;
-  if (p0 >= n) return;
-  const int64_t p1 = std::min(n, p0 + SRANGE);
-  for (int c = threadIdx.x; c < k; c += SBLK) hist[c] = 0;
-  __syncthreads();
-  for (int64_t p = p0 + threadIdx.x; p < p1; p += SBLK) {
-    const int c = key[item_at(items, lo, p)];
-    if ((unsigned)c < (unsigned)k) atomicAdd(&hist[c], 1);
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < k; c += SBLK) {
-    const int h = hist[c];
-    base[c] = h ? atomicAdd(&cur[c], h) : 0;
-    hist[c] = 0;
-  }
-  __syncthreads();
-  for (int64_t p = p0 + threadIdx.x; p < p1; p += SBLK) {
-    const int32_t it = item_at(items, lo, p);
-    const int c = key[it];
-    if ((unsigned)c < (unsigned)k) out[base[c] + atomicAdd(&hist[c], 1)] = it;
+  for (int64_t p0 = (int64_t)blockIdx.x * SRANGE; p0 < n;
+       p0 += (int64_t)gridDim.x * SRANGE) {
+    const int64_t p1 = std::min(n, p0 + SRANGE);
+    __syncthreads();
+    for (int c = threadIdx.x; c < k; c += SBLK) hist[c] = 0;
+    __syncthreads();
+    for (int64_t p = p0 + threadIdx.x; p < p1; p += SBLK) {
+      const int c = key[item_at(items, lo, p)];
+      if ((unsigned)c < (unsigned)k) atomicAdd(&hist[c], 1);
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < k; c += SBLK) {
+      const int h = hist[c];
+      base[c] = h ? atomicAdd(&cur[c], h) : 0;
+      hist[c] = 0;
+    }
+    __syncthreads();
+    for (int64_t p = p0 + threadIdx.x; p < p1; p += SBLK) {
+      const int32_t it = item_at(items, lo, p);
+      const int c = key[it];
+      if ((unsigned)c < (unsigned)k) out[base[c] + atomicAdd(&hist[c], 1)] = it;
+    }
   }
 }
 
@@ -273,10 +279,11 @@ bool sorted_sums_ok(int64_t k, int64_t n, const WsView &v) {
 template <class TX>
 static int launch_seg(const TX *X, int64_t ldx, int d, const int32_t *sorted,
                       int64_t nh, const int32_t *off, int k, double sign,
-                      double *acc, hipStream_t s) {
+                      double *acc, hipStream_t s, bool list = false) {
   const int64_t chunks = (nh + SEG - 1) / SEG;
+  // explicit (moved-sample) lists: a smaller grid, grid-striding
   const int64_t g = std::max<int64_t>(
-      1, std::min<int64_t>((int64_t)cus() * 8,
+      1, std::min<int64_t>((int64_t)cus() * (list ? 2 : 8),
                            (chunks + SUMB / 64 - 1) / (SUMB / 64)));
 #define DKM_SEG(GG, NN)                                                       \
   {                                                                           \
@@ -313,7 +320,12 @@ static int set_sort_lds() {
 static int sort_items(const int32_t *key, const int32_t *items,
                       const int32_t *ndev, int64_t nh, int64_t lo, int k,
                       const WsView &v, hipStream_t s) {
-  const unsigned nb = (unsigned)std::max<int64_t>(1, (nh + SRANGE - 1) / SRANGE);
+  // an explicit list has *ndev <= nh entries, usually few: a fixed grid of
+  // a block per CU strides over whatever it holds (0.06 + 0.56 ms of empty
+  // sort + sum launches per converged C3 iteration on the n-sized grids)
+  const int64_t chunks = (nh + SRANGE - 1) / SRANGE;
+  const unsigned nb = (unsigned)std::max<int64_t>(
+      1, ndev ? std::min<int64_t>(chunks, cus()) : chunks);
   if (hipMemsetAsync(v.scnt, 0, (size_t)k * 4, s) != hipSuccess)
     return fail(DKM_E_LAUNCH, "sorted sums: memset");
   k_sort_count<<<nb, SBLK, (size_t)k * 4, s>>>(key, items, ndev, nh, lo, k,
@@ -339,7 +351,8 @@ static int sort_and_sum(const TX *X, int64_t ldx, int d, const int32_t *key,
                         int64_t lo, int k, double sign, double *acc,
                         const WsView &v, hipStream_t s) {
   if (int r = sort_items(key, items, ndev, nh, lo, k, v, s)) return r;
-  return launch_seg<TX>(X, ldx, d, v.sitems, nh, v.soff, k, sign, acc, s);
+  return launch_seg<TX>(X, ldx, d, v.sitems, nh, v.soff, k, sign, acc, s,
+                        ndev != nullptr);
 }
 
 template <class TX>

@@ -41,8 +41,8 @@ static size_t gemm_bytes(int64_t k, int64_t d) {
   b += round_up(kp * dp * 4, 256);              // gfrag
   b += round_up(kp * dpad64(d) * 2, 256);       // gfrag1
   b += round_up(kp * 4, 256);                   // gcn
-  b += round_up(m * dp * 4, 256);               // gxs
-  b += round_up(m * 4, 256);                    // gxn
+  b += 2 * round_up(m * dp * 4, 256);           // gxs (two chunks)
+  b += 2 * round_up(m * 4, 256);                // gxn (two chunks)
   b += round_up(m * (kp / GT) * GTOP * 8, 256); // gpart
   return b;
 }
@@ -111,6 +111,8 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   v->gcn = nullptr;
   v->gxs = nullptr;
   v->gxn = nullptr;
+  v->gxs1 = nullptr;
+  v->gxn1 = nullptr;
   v->gpart = nullptr;
   v->gchunk = 0;
   v->b1frag = nullptr;
@@ -129,7 +131,11 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
     p += round_up(kp * 4, 256);
     v->gxs = p;
     p += round_up(m * dp * 4, 256);
+    v->gxs1 = p;
+    p += round_up(m * dp * 4, 256);
     v->gxn = (float *)p;
+    p += round_up(m * 4, 256);
+    v->gxn1 = (float *)p;
     p += round_up(m * 4, 256);
     v->gpart = (int2 *)p;
     p += round_up(m * (kp / GT) * GTOP * 8, 256);

@@ -112,6 +112,46 @@ int dkm_assign_delta_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
                          size_t ws_bytes, int32_t *labels, double *delta,
                          int mode, void *stream);
 
+/* The sample image: a resident bf16 copy of X (rows rounded fp64 -> fp32
+ * -> bf16, laid out as the screen's MFMA operands in 32-row tiles) plus
+ * fp32 |x|^2 per row; dkm_x_image_bytes(n, d) bytes (0: d > 128).  Built
+ * once per dataset (it depends only on X), it lets the label-hinted
+ * threshold screen (MODE_SCREEN_BF16 with d <= 128) stream 2 B per feature
+ * instead of 8: labels, sums and re-checks still come from X itself, so
+ * results are identical with or without it.  An image is valid only for the
+ * exact X, n and d it was built from; rebuild it if X changes.  The _img
+ * forms of dkm_partial_sum / dkm_assign_delta take it (NULL = none); every
+ * other argument is theirs.  Same interface as base.py:166-181.            */
+size_t dkm_x_image_bytes(int64_t n, int64_t d);
+/* 1 when the screen that (k, d, mode) selects reads a sample image (the
+ * label-hinted single-product screen, MODE_SCREEN_BF16 or the AUTO choice
+ * for sums beyond LDS), else 0: building one would be wasted.            */
+int dkm_x_image_useful(int64_t k, int64_t d, int mode);
+int dkm_x_image_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
+                    void *image, size_t image_bytes, void *stream);
+int dkm_x_image_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
+                    void *image, size_t image_bytes, void *stream);
+int dkm_partial_sum_img_f64(const double *X, const void *image, int64_t n,
+                            int64_t d, int64_t ldx, const double *C,
+                            int64_t k, const void *ws, size_t ws_bytes,
+                            int32_t *labels, double *acc, int mode,
+                            void *stream);
+int dkm_partial_sum_img_f32(const float *X, const void *image, int64_t n,
+                            int64_t d, int64_t ldx, const double *C,
+                            int64_t k, const void *ws, size_t ws_bytes,
+                            int32_t *labels, double *acc, int mode,
+                            void *stream);
+int dkm_assign_delta_img_f64(const double *X, const void *image, int64_t n,
+                             int64_t d, int64_t ldx, const double *C,
+                             int64_t k, const void *ws, size_t ws_bytes,
+                             int32_t *labels, double *delta, int mode,
+                             void *stream);
+int dkm_assign_delta_img_f32(const float *X, const void *image, int64_t n,
+                             int64_t d, int64_t ldx, const double *C,
+                             int64_t k, const void *ws, size_t ws_bytes,
+                             int32_t *labels, double *delta, int mode,
+                             void *stream);
+
 /* y[i] += x[i] (device, fp64): acc_new = acc_old + delta.                  */
 int dkm_add_f64(double *y, const double *x, int64_t n, void *stream);
 /* The same, and *nonzero (device int32) <- 1 if any x[i] != 0, else 0:

@@ -3,7 +3,8 @@ screen: k_screen_b2 (centres on the lanes, dkm_b2.hip) and the k_screen_b1
 it replaces (DKM_B1_LEGACY=1), against the oracle's restatement of the
 reference assignment (dislib cluster/kmeans/base.py:171-173, 204-205).
 
-Shapes cover every K-step count the kernels instantiate that the LDS admits,
+The image variant also checks the image itself against the fp64 -> fp32 ->
+bf16 roundings (test_sample_image_layout).  Shapes cover every K-step count the kernels instantiate that the LDS admits,
 k % 32 != 0 (hints pointing into a partial last block), an odd number of
 centre blocks (the pipeline's tail), k > 1024 (own masks of several words),
 and a shape whose b2 image does not fit LDS (the b1 fallback).  Hint kinds:
@@ -28,15 +29,14 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.fixture(params=["b2", "b1"])
-def variant(request):
-    old = os.environ.get("DKM_B1_LEGACY")
-    os.environ["DKM_B1_LEGACY"] = "1" if request.param == "b1" else "0"
+@pytest.fixture(params=["img", "b2", "b1"])
+def variant(request, monkeypatch):
+    """img: k_screen_b2 streaming the sample image (the fit's default);
+    b2: the same kernel converting X itself; b1: k_screen_b1."""
+    from dislib_amd import _device
+    monkeypatch.setenv("DKM_B1_LEGACY", "1" if request.param == "b1" else "0")
+    monkeypatch.setattr(_device, "X_IMAGE", request.param == "img")
     yield request.param
-    if old is None:
-        os.environ.pop("DKM_B1_LEGACY", None)
-    else:
-        os.environ["DKM_B1_LEGACY"] = old
 
 
 def _hinted(x, C, hint, acc_kind="partial"):
@@ -201,3 +201,36 @@ def test_refresh_skipped_once_converged(monkeypatch):
                  np.maximum(np.abs(ref.centers), 1.0))
     assert err <= 1e-9
     assert 1 <= len(calls) < 7, len(calls)
+
+
+@pytest.mark.parametrize("n,d", [(1000, 64), (77, 20), (33, 128), (64, 1)])
+def test_sample_image_layout(n, d):
+    """dkm_x_image_f64: 32-row tiles of dpad16(d) / 16 K-steps; lane l of
+    K-step ks holds row l & 31, features 16 ks + 8 (l >> 5) + 0..7, rounded
+    fp64 -> fp32 -> bf16 (nearest even); rows and features past n, d zero;
+    then fp32 |x|^2 of the fp32 values per row (32 per tile)."""
+    from dislib_amd import _device, _lib
+    so = _lib.lib()
+    rng = np.random.default_rng(n + d)
+    x = rng.standard_normal((n, d)) * 10.0 ** rng.integers(-3, 4, (n, 1))
+    X = torch.from_numpy(x).cuda()
+    nb = so.dkm_x_image_bytes(n, d)
+    nt, nks = (n + 31) // 32, (d + 15) // 16
+    assert nb == nt * nks * 1024 + nt * 128
+    img = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+    _lib.check(so.dkm_x_image_f64(_device.ptr(X), n, d, d, _device.ptr(img),
+                                  nb, _device.stream_ptr()), "image")
+    raw = img.cpu().numpy()
+    tiles = raw[:nt * nks * 1024].view(np.uint16).reshape(nt, nks, 64, 8)
+    xx = raw[nt * nks * 1024:].view(np.float32)
+    # fp32 -> bf16 round to nearest even (finite values)
+    f = np.zeros((nt * 32, nks * 16), np.float32)
+    f[:n, :d] = x.astype(np.float32)
+    u = f.view(np.uint32).astype(np.uint64)
+    bf = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    bf = bf.reshape(nt, 32, nks, 2, 8)            # tile, row, ks, half, j
+    want = bf.transpose(0, 2, 3, 1, 4).reshape(nt, nks, 64, 8)
+    assert np.array_equal(tiles, want)
+    ref = (f.astype(np.float64) ** 2).sum(1)
+    assert np.all(np.abs(xx - ref) <= 2.0 ** -23 * ref)
+    assert np.all(xx[n:] == 0)

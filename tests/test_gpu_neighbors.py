@@ -84,6 +84,23 @@ def test_kneighbors_ties_by_index():
     assert np.array_equal(ind, oi) and np.array_equal(dist, od)
 
 
+def test_kneighbors_overflowed_distances_fill_the_list():
+    """Fewer finite rows than n_neighbors: rows whose squared distance
+    overflows to +inf still fill the list (sklearn returns them too), as
+    real fit indices with distance inf, never a sentinel."""
+    rng = np.random.default_rng(11)
+    xf = rng.standard_normal((40, 3))
+    xf[3:] = 1e200 * (1.0 + rng.random((37, 3)))   # (1e200)^2 = inf
+    xq = rng.standard_normal((5, 3))
+    dist, ind = _knn(xf, xq, 40, 8, 5)
+    od, oi = orc.kneighbors_exact(xf[:3], xq, 3)
+    assert np.array_equal(ind[:, :3], oi) and np.array_equal(dist[:, :3], od)
+    assert np.all(np.isinf(dist[:, 3:]))
+    assert np.all((ind[:, 3:] >= 3) & (ind[:, 3:] < 40))
+    for row in ind:
+        assert len(set(row.tolist())) == 8
+
+
 def test_kneighbors_return_indices_only_and_device_data():
     from dislib_amd.data import load_data
     from dislib_amd.neighbors import NearestNeighbors
@@ -135,6 +152,7 @@ def test_epsilon_query_reference_golden(name):
     (500, 100, 14.0, 30, 480, False),   # d > 64: query read from memory
     (1500, 2, 1.5, 0, 1500, True),      # integer grid: many equal distances
     (6000, 2, 1e9, 0, 3, False),        # lists of 6000 (> LDS sort cap)
+    (21000, 2, 1e9, 0, 3, True),        # 6 runs, 3 merge passes, ties
     (800, 2, 2.0, 0, 800, True),        # distances exactly eps (excluded)
     (300, 3, 0.0, 0, 300, True),        # eps = 0: no neighbours at all
     (300, 3, -1.0, 0, 300, False),      # negative eps: none either
