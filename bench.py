@@ -257,10 +257,22 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
            "pred_ms": pred_ms,
            "collective": ("libdkm-rccl" if info else "torch.distributed")
            if world > 1 else "none",
-           "rccl_ranks": info[0] if info else None}
+           "rccl_ranks": info[0] if info else None,
+           "pruned": st.pstate is not None,
+           # samples screened per pruned iteration (whole fit; the first is
+           # the bounds' initial full pass)
+           "active": list(st.active)}
     del st, ds, X
     torch.cuda.empty_cache()
     return out
+
+
+def prune_fields(r, n):
+    """Bound-based skipping (dkm_assign_pruned): samples screened per pruned
+    iteration of the whole fit, as fractions of the shard."""
+    if not r.get("pruned"):
+        return None
+    return {"screened_frac": [round(a / n, 5) for a in r["active"]]}
 
 
 def fit_fields(r, n, world):
@@ -425,7 +437,8 @@ def main():
              "steps": steps, "warmup": warm,
              "roofline": roofline(n, d, k, rr, False, 4 if f32 else 8,
                                   csr_nnz=nnz),
-             "rechecked_samples": rr["rechecked"]}
+             "rechecked_samples": rr["rechecked"],
+             "pruning": prune_fields(rr, n)}
         e.update(fit_fields(rr, n, world))
         if nnz:
             e["nnz_per_row"] = nnz
@@ -479,6 +492,7 @@ def main():
                    "parallelism": "dp%d" % world},
         "roofline": rf,
         "rechecked_samples": r["rechecked"],
+        "pruning": prune_fields(r, a.n),
         "collective": r["collective"],
     }
     out.update(fit_fields(r, a.n, world))

@@ -268,6 +268,50 @@ def assign_delta(dd, C, ws, labels, delta, mode):
                "dkm_assign_delta")
 
 
+def prune_supported(dd, k):
+    so = _lib.lib()
+    return (not dd.sparse and dd.n > 0 and
+            bool(so.dkm_prune_supported(int(k), dd.d)))
+
+
+class PruneState:
+    """Caller-owned state of dkm_assign_pruned_* (per-sample distance
+    bounds, active list, gather block) for one fit on one DeviceData."""
+
+    def __init__(self, dd, k):
+        t = torch()
+        so = _lib.lib()
+        self.nbytes = int(so.dkm_prune_state_bytes(dd.n, int(k), dd.d))
+        self.buf = t.empty(self.nbytes, dtype=t.uint8, device=dd.device)
+        self.valid = False       # bounds written by a previous call
+
+
+def assign_pruned(dd, C, C_prev, ws, labels, delta, st):
+    """dkm_assign_pruned_*: labels in/out, delta +=; returns the number of
+    samples screened (the others' labels are proven unchanged)."""
+    so = _lib.lib()
+    k = C.shape[0]
+    img = dd.screen_image(k, _lib.MODE_BF16)
+    fn = so.dkm_assign_pruned_f32 if dd.dtype == np.float32 else \
+        so.dkm_assign_pruned_f64
+    na = ctypes.c_int64(0)
+    _lib.check(fn(ptr(dd.X), ptr(img), dd.n, dd.d, dd.X.stride(0), ptr(C),
+                  ptr(C_prev), k, ws.p, ws.nbytes, ptr(labels), ptr(delta),
+                  ptr(st.buf), st.nbytes, 0 if st.valid else 1,
+                  ctypes.byref(na), stream_ptr()), "dkm_assign_pruned")
+    st.valid = True
+    return int(na.value)
+
+
+def label_sums(dd, ws, labels, acc, k):
+    """acc += [sums | counts] of X by labels (dkm_label_sums_*)."""
+    so = _lib.lib()
+    fn = so.dkm_label_sums_f32 if dd.dtype == np.float32 else \
+        so.dkm_label_sums_f64
+    _lib.check(fn(ptr(dd.X), dd.n, dd.d, dd.X.stride(0), ptr(labels), int(k),
+                  ws.p, ws.nbytes, ptr(acc), stream_ptr()), "dkm_label_sums")
+
+
 def add_(y, x, nonzero=None):
     """y += x; with ``nonzero`` (a device int32 element view): 1 there if any
     x != 0, else 0."""

@@ -50,6 +50,18 @@ SIGNATURES = {
                                         _p, _sz, _p, _p, _i32, _p]),
     "dkm_assign_delta_img_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _i64,
                                         _p, _sz, _p, _p, _i32, _p]),
+    "dkm_prune_state_bytes": (_sz, [_i64, _i64, _i64]),
+    "dkm_prune_supported": (_i32, [_i64, _i64]),
+    "dkm_assign_pruned_f64": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, _i64,
+                                     _p, _sz, _p, _p, _p, _sz, _i32,
+                                     ctypes.POINTER(_i64), _p]),
+    "dkm_assign_pruned_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, _i64,
+                                     _p, _sz, _p, _p, _p, _sz, _i32,
+                                     ctypes.POINTER(_i64), _p]),
+    "dkm_label_sums_f64": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz,
+                                  _p, _p]),
+    "dkm_label_sums_f32": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz,
+                                  _p, _p]),
     "dkm_add_f64": (_i32, [_p, _p, _i64, _p]),
     "dkm_add_f64_nz": (_i32, [_p, _p, _i64, _p, _p]),
     "dkm_predict_f64": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz, _p,

@@ -150,6 +150,15 @@ class KMeans:
 # assignment (a converged fit stops re-reading X for them).
 REFRESH = int(os.environ.get("DKM_REFRESH", "8"))
 
+# Bound-based skipping (dkm_assign_pruned_*, dkm_prune.hip): from the second
+# iteration on, samples whose distance bounds prove their label unchanged
+# are not screened.  Labels are identical either way.  Opt-in (DKM_PRUNE=1):
+# on the C3 shard the bf16 screen's bounds leave 12-39 % of the samples
+# active through iteration 10 (the fit's centres crowd), and the bounds
+# pass, gather and tier-2 re-reads made the iterations slower than
+# screening everything (profiles/r03/prune/).
+PRUNE = os.environ.get("DKM_PRUNE", "0") == "1"
+
 
 class _Lloyd:
     """Device state of one fit: resident data, centres, labels, workspace and
@@ -206,6 +215,15 @@ class _Lloyd:
         # every rank must refresh on the same iterations (their delta states
         # are summed): rank 0's setting wins
         self.refresh = _shard.broadcast_int(REFRESH, dd.device)
+        from .._device import prune_supported
+        self.pstate = None
+        self.C_prev = None
+        self.active = []          # samples screened per pruned iteration
+        if (PRUNE and mode in ("auto", "bf16") and
+                prune_supported(dd, k)):
+            from .._device import PruneState
+            self.pstate = PruneState(dd, k)
+            self.C_prev = t.empty_like(self.C)
 
     def prepare(self):
         """Per-iteration centre data + zeroed accumulator."""
@@ -230,12 +248,27 @@ class _Lloyd:
         if mode == _lib.MODE_AUTO and self.it == 0:
             mode = _lib.MODE_BF16X3
         with self._on():
-            if self._full():
+            if self.pstate is not None and self.it > 0:
+                self._pruned()
+            elif self._full():
                 partial_sum(self.dd, self.C, self.ws, self.labels, self.acc,
                             mode)
             else:
                 assign_delta(self.dd, self.C, self.ws, self.labels, self.acc,
                              mode)
+
+    def _pruned(self):
+        """Incremental assignment with bound-based skipping; on a refresh
+        iteration the sums are then recomputed from the labels."""
+        from .._device import assign_pruned, label_sums
+        na = assign_pruned(self.dd, self.C, self.C_prev, self.ws, self.labels,
+                           self.acc, self.pstate)
+        self.active.append(na)
+        self.C_prev.copy_(self.C)
+        if self._full():
+            self.acc.zero_()
+            label_sums(self.dd, self.ws, self.labels[:self.dd.n], self.acc,
+                       self.k)
 
     def assign(self):
         self.prepare()

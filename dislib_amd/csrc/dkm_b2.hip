@@ -59,6 +59,11 @@ constexpr int SB2 = DKM_AB_SB2;
 constexpr uint32_t PACK2 = 9, PACK2_MASK = (1u << PACK2) - 1;
 constexpr int B2_ENT = 3;    // kept (score, centre) per sample besides p
 constexpr int B2_RTHR = 4;   // over-full samples a wave tolerates per tile
+// bounds mode (B2View::bnd): the threshold is raised by M = min(B2_MU d_p^2,
+// mag) per row for a "near" test, so a row with no centre in (T, T + M]
+// gets a second-best lower bound M above its own distance (dkm_prune.hip)
+constexpr float B2_MU = 3.0f;
+constexpr int B2_NEAR = 0x10000;  // s_cnt flag: a centre within T + M
 // per-wave LDS scratch: -T[32], hint[32], count[32], |x|^2[32], the tile
 // transpose (32 rows x 16 bf16 features, 1 KB; the kept entries
 // [32][B2_ENT] reuse it after the tile's conversion), then 32 x nkw
@@ -105,6 +110,10 @@ struct B2View {
   int2 *tlist, *clist;
   int4 *nlist;
   int32_t *tcount, *ccount, *ncount;
+  // bounds mode: per row (upper bound on the distance to the final label,
+  // lower bound on every other centre's if that label is .w, else the
+  // third) -- see dkm_prune.hip; nullptr = off
+  float4 *bnd;
 };
 
 template <class TX, int NKS, bool W1, bool PC, bool IMG>
@@ -150,7 +159,8 @@ __global__ void __launch_bounds__(SB2)
   bk.k_mag = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(
       2.0f * (2.0f * rel + 0x1.0p-23f * (float)(1u << PACK2)) * 1.0001f)));
   // threshold pass: no packing, the chain over |T| + sum |x c| (see top)
-  const float relt = 1.02f * 0x1.0p-8f + (32.0f * NKS + 16.0f) * 0x1.0p-23f;
+  // (the chain starts from -(T + M), M <= mag: magnitudes <= 3.04 mag)
+  const float relt = 1.02f * 0x1.0p-8f + (48.0f * NKS + 32.0f) * 0x1.0p-23f;
   BoundK bkt = bk;
   bkt.k_mag = __int_as_float(__builtin_amdgcn_readfirstlane(
       __float_as_int(2.0f * (2.0f * relt) * 1.0001f)));
@@ -175,6 +185,7 @@ __global__ void __launch_bounds__(SB2)
   int *s_hp = (int *)(scr + 128);          // hint per sample (-1: none)
   int *s_cnt = (int *)(scr + 256);         // kept entries appended
   float *s_xx = (float *)(scr + 384);      // |x|^2 per sample
+  float *s_m = s_xx;                        // M per sample, in process()
   char *s_tx = scr + 512;                   // one K-step of the tile, bf16
   int2 *s_ent = (int2 *)(scr + 512);       // (score bits, centre), later
   uint32_t *s_om =
@@ -272,6 +283,20 @@ __global__ void __launch_bounds__(SB2)
     int i1 = 0, i2 = 0;
     uint32_t mpk0 = 0, mpk1 = 0, mpk2 = 0;  // many: the candidate set
     bool need3 = true;
+    // bounds mode: distance bounds from squared-score bounds, each with a
+    // 2^-20 relative margin (the fp32 evaluation, the sqrt, and the
+    // reference's own fp64 rounding); |x|^2 from fp32 within 2^-14
+    float bu = INFINITY, bl1 = -INFINITY, bl0 = -INFINITY;
+    int bi = 0;
+    const float xxh = xx * (1.0f + 0x1.0p-14f), xxl = xx * (1.0f - 0x1.0p-14f);
+    auto ub_of = [](float q2) {
+      const float q = __builtin_sqrtf(fmaxf(q2, 0.f));
+      return q + q * 0x1.0p-20f;
+    };
+    auto lb_of = [](float q2) {
+      const float q = __builtin_sqrtf(fmaxf(q2, 0.f));
+      return q - q * 0x1.0p-20f;
+    };
     if (hint) {
       const bool pok = prv >= 0 && prv < k && si < n;
       const uint64_t bad = __ballot(!pok && si < n);
@@ -322,12 +347,18 @@ __global__ void __launch_bounds__(SB2)
         const float ncp = ncn[p];
         const float sp = dg - ncp;  // s_hat_p = |c_p|^2 + x.(-2 c_p)
         const float T = pok ? sp + B2t : -INFINITY;
+        float Mr = 0.f;  // bounds mode: the near-test margin of row r
+        if (v.bnd && pok) {
+          const float magr = fmaf(xn, bkt.two_cm, bkt.cm2);
+          Mr = fminf(B2_MU * fmaxf(xx + sp, 0.f), magr);
+        }
         // ---- per-wave scratch: -T, hints, counts, own masks --------------
         wave_sync();
         if (h == 0) {
-          s_tn[r] = -T;
+          s_tn[r] = -(T + Mr);
           s_hp[r] = pok ? p : -1;
           s_cnt[r] = 0;
+          s_m[r] = Mr;
         }
         for (int w = lane; w < 32 * nkw; w += 64) s_om[w] = 0u;
         wave_sync();
@@ -358,8 +389,16 @@ __global__ void __launch_bounds__(SB2)
           pg[4 * q + 3] = p4.w;
         }
         const uint32_t om0 = s_om[r];
+        // bounds mode: kept iff within T (the score + M test passed too);
+        // within (T, T + M] only flags the row as near
+        auto keep = [&](int row, float a, float t) {
+          const bool k2 = a + s_m[row] <= t;
+          if (!k2) atomicOr(&s_cnt[row], B2_NEAR);
+          return k2;
+        };
         auto push = [&](int row, float s, int j) {
-          const int slot = atomicAdd(&s_cnt[row], 1);
+          // (the count is the low half: the near flag may be set)
+          const int slot = atomicAdd(&s_cnt[row], 1) & (B2_NEAR - 1);
           if (slot < B2_ENT)
             s_ent[row * B2_ENT + slot] = make_int2(__float_as_int(s), j);
         };
@@ -375,8 +414,10 @@ __global__ void __launch_bounds__(SB2)
           if (pok && !dup && m <= ncp) {
 #pragma unroll
             for (int g = 0; g < 16; ++g)
-              if (pg[g] != p && dn[g] + cin[g] <= ncp)
-                push((g & 3) + 8 * (g >> 2) + 4 * h, dn[g] - ncp, p);
+              if (pg[g] != p && dn[g] + cin[g] <= ncp) {
+                const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
+                if (keep(row, dn[g] + cin[g], ncp)) push(row, dn[g] - ncp, p);
+              }
           }
         }
         // ---- all centre blocks: lane = centre, registers = samples -------
@@ -422,8 +463,11 @@ __global__ void __launch_bounds__(SB2)
             const int j = cb * 32 + r;
 #pragma unroll
             for (int g = 0; g < 16; ++g)
-              if (acc[g] <= thr)
-                push((g & 3) + 8 * (g >> 2) + 4 * h, (acc[g] - cin[g]) - nc, j);
+              if (acc[g] <= thr) {
+                const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
+                if (keep(row, acc[g], thr))
+                  push(row, (acc[g] - cin[g]) - nc, j);
+              }
           }
         };
         if (DKM_AB_B2_PROBE != 1) {
@@ -479,7 +523,9 @@ __global__ void __launch_bounds__(SB2)
         }
         // ---- decision over the hint and the kept entries ------------------
         wave_sync();
-        const int cnt = s_cnt[r];
+        const int craw = s_cnt[r];
+        const int cnt = craw & (B2_NEAR - 1);
+        const bool nearr = craw >= B2_NEAR;
         float sv[B2_ENT + 1];
         int cv[B2_ENT + 1];
         bool ok[B2_ENT + 1];
@@ -491,7 +537,8 @@ __global__ void __launch_bounds__(SB2)
           const int2 en = s_ent[r * B2_ENT + e];
           sv[e + 1] = __int_as_float(en.x);
           cv[e + 1] = en.y;
-          ok[e + 1] = e < cnt;
+          // (an index outside [0, k) never reaches the candidate kernels)
+          ok[e + 1] = e < cnt && (unsigned)en.y < (unsigned)k;
         }
         const bool over = cnt > B2_ENT || !pok || !sane0 || !(T < 1e30f);
         float bs = INFINITY;
@@ -530,6 +577,21 @@ __global__ void __launch_bounds__(SB2)
           mpk0 = pk[0];
           mpk1 = pk[1];
           mpk2 = pk[2];
+          if (v.bnd && !over) {
+            // every centre outside the kept set K = {p} + entries has
+            // s_j > s_hat_p + B2t / 2 (+ M unless the row is near); inside
+            // K, s_j >= its score - B2t.  The final label is bc unless the
+            // exact re-check picks another member of K.
+            float m2 = INFINITY;
+#pragma unroll
+            for (int e = 0; e <= B2_ENT; ++e)
+              if (ok[e] && !(sv[e] == bs && cv[e] == bc)) m2 = fminf(m2, sv[e]);
+            const float base = sp + 0.25f * B2t + (nearr ? 0.f : 0.99f * Mr);
+            bu = ub_of(xxh + bs + B2t);
+            bl1 = lb_of(xxl + fminf(base, m2 - B2t));
+            bl0 = lb_of(xxl + fminf(base, bs - B2t));
+            bi = bc;
+          }
         }
       }
     }
@@ -635,12 +697,21 @@ __global__ void __launch_bounds__(SB2)
         ins3(o3, j3);
       }
       const bool sane = sane0 & (r1 < 1e30f);
+      if (v.bnd && sane) {
+        // packed scores: within B2 / 2 each (the packing included)
+        bu = ub_of(xxh + r1 + B2);
+        bl1 = lb_of(xxl + r2 - B2);
+        bl0 = lb_of(xxl + r1 - B2);
+        bi = ii1;
+      }
       unique = sane & (r2 - r1 > B2);
       two = sane & !unique & (r3 - r1 > B2);
       i1 = ii1;
       i2 = ii2;
     }
     const bool valid = si < n && h == 0;
+    if (v.bnd && valid)
+      v.bnd[si - base] = make_float4(bu, bl1, bl0, __int_as_float(bi));
     const int prev = delta ? prv : -1;
     // 3..6 candidates of the threshold pass -> the N-candidate list
     bool nlisted = false;
@@ -1012,7 +1083,8 @@ template int launch_x_image<float>(const float *, int64_t, int, int64_t,
 template <class TX>
 int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
                      const WsView &v, int32_t *lab_out, int64_t base, int hint,
-                     int cus, hipStream_t s, int *nseg, XImage img) {
+                     int cus, hipStream_t s, int *nseg, XImage img,
+                     float4 *bnd) {
   const bool pc = b2pc_enabled() && SB2 / 64 > B2_NLOAD &&
                   b2pc_lds_bytes(k, d) <= 160 * 1024;
   const size_t lds = pc ? b2pc_lds_bytes(k, d) : b2_lds_bytes(k, d);
@@ -1061,6 +1133,7 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
   bv.tcount = v.tcount;
   bv.ccount = v.ccount;
   bv.ncount = v.ncount;
+  bv.bnd = bnd;
   hipLaunchKernelGGL((void (*)(const TX *, int64_t, int, int64_t, int, B2View,
                                int32_t *, int64_t, int, int, XImage))kf,
                      dim3(g), dim3(SB2), lds, s, X, end, d, ldx, k, bv,
@@ -1071,9 +1144,11 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
 
 template int launch_screen_b2<double>(const double *, int64_t, int, int64_t,
                                       int, const WsView &, int32_t *, int64_t,
-                                      int, int, hipStream_t, int *, XImage);
+                                      int, int, hipStream_t, int *, XImage,
+                                      float4 *);
 template int launch_screen_b2<float>(const float *, int64_t, int, int64_t, int,
                                      const WsView &, int32_t *, int64_t, int,
-                                     int, hipStream_t, int *, XImage);
+                                     int, hipStream_t, int *, XImage,
+                                     float4 *);
 
 }  // namespace dkm

@@ -2693,7 +2693,8 @@ template <class TX>
 static int launch_screen(int prec, const TX *X, int64_t n, int d,
                          int64_t ldx, const double *C, int k, const WsView &v,
                          size_t wsb, int32_t *labels, double *acc,
-                         int acc_kind, hipStream_t s, XImage img) {
+                         int acc_kind, hipStream_t s, XImage img,
+                         float4 *bnd = nullptr) {
   (void)wsb;
   const int64_t nq = std::min<int64_t>(v.nq, INT32_MAX);
   if (!labels && nq < 1)
@@ -2706,6 +2707,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const bool b1 = prec == P_B1 && v.b1frag && vec &&
                   (int64_t)32 * ldx * (int64_t)sizeof(TX) < (1ll << 31) &&
                   (acc_kind == 0 || acc_kind == 1 || (labels && nq >= n));
+  if (bnd && !b1)
+    return fail(DKM_E_ARG, "screen: bounds need the single-product screen");
   if (prec == P_B1 && !b1) prec = P_B3;
   // d <= 32 bf16x3 with the 32x32x16 fragments resident: k_screen_w32
   const size_t fb32 = (size_t)(kpad32(k) / 32) * (4096 + 128);
@@ -2747,8 +2750,10 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
       const int hint = labels && acc_kind != 0 ? 1 : 0;
       r = b2_enabled() ? launch_screen_b2<TX>(X, end, d, ldx, k, v, lab_out,
                                               base, hint, dev_info().cus, s,
-                                              &nseg, img)
+                                              &nseg, img, bnd)
                        : 1;
+      if (r == 1 && bnd)
+        return fail(DKM_E_ARG, "screen: bounds need k_screen_b2");
       if (r == 1)
         r = launch_screen_b1<TX>(X, end, d, ldx, k, v, lab_out, base, hint, s,
                                  &nseg);
@@ -2891,6 +2896,96 @@ static int x_image(const TX *X, int64_t n, int64_t d, int64_t ldx,
                             (hipStream_t)stream);
 }
 
+// ---- dkm_assign_pruned_*: bound-based skipping (dkm_prune.hip) ----------
+static bool prune_ok(int64_t k, int64_t d) {
+  return d <= 128 && d % 8 == 0 && k >= 2 && k <= INT32_MAX &&
+         !gemm_path(k, d) && screen_ok(k, d) && b1_ok(k, d) && b2_enabled() &&
+         b2_lds_bytes(k, d) <= 160 * 1024;
+}
+
+template <class TX>
+static int assign_pruned(const TX *X, const void *image, int64_t n, int64_t d,
+                         int64_t ldx, const double *C, const double *Cp,
+                         int64_t k, const void *ws, size_t wsb,
+                         int32_t *labels, double *delta, void *state,
+                         size_t sb, int init, int64_t *n_active, void *stream,
+                         const char *who) {
+  const std::string w(who);
+  if (n < 0 || d <= 0 || k <= 0 || ldx < d) return fail(DKM_E_ARG, w + ": bad n/d/k/ldx");
+  if (!labels || !delta || !state || !C || (!init && !Cp))
+    return fail(DKM_E_ARG, w + ": NULL argument");
+  if (!prune_ok(k, d))
+    return fail(DKM_E_ARG, w + ": needs the single-product screen "
+                               "(d <= 128, d % 8 == 0, k x d within LDS)");
+  if (((uintptr_t)X % 16) != 0 || ldx % (16 / (int64_t)sizeof(TX)) != 0 ||
+      (int64_t)32 * ldx * (int64_t)sizeof(TX) >= (1ll << 31))
+    return fail(DKM_E_ARG, w + ": X rows must be 16-B aligned");
+  if (sb < prune_state_bytes(n, k, d))
+    return fail(DKM_E_WORKSPACE, w + ": state buffer too small");
+  if (n_active) *n_active = 0;
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  WsView v;
+  if (int r = ws_view(ws, wsb, k, d, &v)) return r;
+  const PruneView p = prune_view(state, n, k, d);
+  int64_t na = n;
+  if (!init) {
+    if (int r = launch_prune<TX>(X, ldx, C, Cp, k, d, labels, p, s)) return r;
+    if (hipMemcpyAsync(&na, p.bcnt + p.nb, 8, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return fail(DKM_E_LAUNCH, w + ": active count");
+  }
+  if (n_active) *n_active = na;
+  const int64_t cap = std::min<int64_t>(p.cap, v.nq) / 32 * 32;
+  if (cap < 32) return fail(DKM_E_WORKSPACE, w + ": label scratch too small");
+  // most samples active: screen X in place (through the image when given)
+  const bool gather = !init && na * 5 <= n * 2;
+  const int64_t total = gather ? na : n;
+  const int nks = (int)(dpad16(d) / 16);
+  const XImage img0 =
+      image ? x_image_view(image, n, d) : XImage{nullptr, nullptr};
+  for (int64_t j0 = 0; j0 < total; j0 += cap) {
+    const int64_t m = std::min(cap, total - j0);
+    const TX *Xc;
+    int64_t ldc;
+    int32_t *lc;
+    XImage img{nullptr, nullptr};
+    if (gather) {
+      if (int r = launch_prune_gather<TX>(X, ldx, (int)d, p, j0, m, labels, s))
+        return r;
+      Xc = (const TX *)p.xa;
+      ldc = d;
+      lc = p.la;
+    } else {
+      Xc = X + j0 * ldx;
+      ldc = ldx;
+      lc = labels + j0;
+      if (img0.tiles)
+        img = XImage{img0.tiles + (j0 / 32) * nks * 512, img0.xx + j0};
+    }
+    if (int r = launch_screen<TX>(P_B1, Xc, m, (int)d, ldc, C, (int)k, v, wsb,
+                                  lc, delta, 2, s, img, p.bnd))
+      return r;
+    if (int r = launch_prune_final(gather, p, j0, m, lc, labels, s)) return r;
+  }
+  return 0;
+}
+
+template <class TX>
+static int label_sums_abi(const TX *X, int64_t n, int64_t d, int64_t ldx,
+                          const int32_t *labels, int64_t k, const void *ws,
+                          size_t wsb, double *acc, void *stream) {
+  if (n < 0 || d <= 0 || k <= 0 || ldx < d || d > INT32_MAX || k > INT32_MAX)
+    return fail(DKM_E_ARG, "label_sums: bad n/d/k/ldx");
+  if (n == 0) return 0;
+  if (!X || !labels || !acc) return fail(DKM_E_ARG, "label_sums: NULL");
+  WsView v;
+  if (int r = ws_view(ws, wsb, k, d, &v)) return r;
+  return launch_post_sums<TX>(X, 0, n, (int)d, ldx, labels, nullptr, (int)k,
+                              acc, v, (hipStream_t)stream);
+}
+
 }  // namespace dkm
 
 using namespace dkm;
@@ -3016,6 +3111,49 @@ int dkm_assign_delta_img_f32(const float *X, const void *image, int64_t n,
     return fail(DKM_E_ARG, "assign_delta: labels and delta are required");
   return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, delta, 2,
                        mode, stream, "dkm_assign_delta_img_f32", image);
+}
+
+size_t dkm_prune_state_bytes(int64_t n, int64_t k, int64_t d) {
+  if (n < 0 || k <= 0 || d <= 0) return 0;
+  return prune_state_bytes(n, k, d);
+}
+
+int dkm_prune_supported(int64_t k, int64_t d) { return prune_ok(k, d) ? 1 : 0; }
+
+int dkm_assign_pruned_f64(const double *X, const void *image, int64_t n,
+                          int64_t d, int64_t ldx, const double *C,
+                          const double *C_prev, int64_t k, const void *ws,
+                          size_t ws_bytes, int32_t *labels, double *delta,
+                          void *state, size_t state_bytes, int init,
+                          int64_t *n_active, void *stream) {
+  return assign_pruned<double>(X, image, n, d, ldx, C, C_prev, k, ws, ws_bytes,
+                               labels, delta, state, state_bytes, init,
+                               n_active, stream, "dkm_assign_pruned_f64");
+}
+
+int dkm_assign_pruned_f32(const float *X, const void *image, int64_t n,
+                          int64_t d, int64_t ldx, const double *C,
+                          const double *C_prev, int64_t k, const void *ws,
+                          size_t ws_bytes, int32_t *labels, double *delta,
+                          void *state, size_t state_bytes, int init,
+                          int64_t *n_active, void *stream) {
+  return assign_pruned<float>(X, image, n, d, ldx, C, C_prev, k, ws, ws_bytes,
+                              labels, delta, state, state_bytes, init,
+                              n_active, stream, "dkm_assign_pruned_f32");
+}
+
+int dkm_label_sums_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
+                       const int32_t *labels, int64_t k, const void *ws,
+                       size_t ws_bytes, double *acc, void *stream) {
+  return label_sums_abi<double>(X, n, d, ldx, labels, k, ws, ws_bytes, acc,
+                                stream);
+}
+
+int dkm_label_sums_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
+                       const int32_t *labels, int64_t k, const void *ws,
+                       size_t ws_bytes, double *acc, void *stream) {
+  return label_sums_abi<float>(X, n, d, ldx, labels, k, ws, ws_bytes, acc,
+                               stream);
 }
 
 int dkm_add_f64(double *y, const double *x, int64_t n, void *stream) {

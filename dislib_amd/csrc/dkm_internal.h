@@ -164,7 +164,35 @@ template <class TX>
 int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
                      const WsView &v, int32_t *lab_out, int64_t base,
                      int hint, int cus, hipStream_t s, int *nseg,
-                     XImage img);
+                     XImage img, float4 *bnd = nullptr);
+
+// Bound-based skipping of samples whose label cannot change
+// (dkm_prune.hip; the state buffer of dkm_assign_pruned_*).
+struct PruneView {
+  int64_t n, nb, cap;
+  float2 *ul;      // n (upper, lower) distance bounds
+  int32_t *act;    // n active sample indices
+  uint64_t *mask;  // ceil(n / 64) active bits
+  int64_t *bcnt;   // nb + 1 range counts / offsets (bcnt[nb] = total)
+  float *drift;    // kpad32 centre moves
+  float *dstat;    // max move, second max, argmax (int bits)
+  char *xa;        // cap gathered rows (TX, ld = d)
+  int32_t *la;     // cap gathered labels
+  float4 *bnd;     // cap bounds from k_screen_b2
+};
+size_t prune_state_bytes(int64_t n, int64_t k, int64_t d);
+PruneView prune_view(void *state, int64_t n, int64_t k, int64_t d);
+template <class TX>
+int launch_prune(const TX *X, int64_t ldx, const double *C, const double *Cp,
+                 int64_t k, int64_t d, const int32_t *lab, const PruneView &p,
+                 hipStream_t s);
+template <class TX>
+int launch_prune_gather(const TX *X, int64_t ldx, int d, const PruneView &p,
+                        int64_t j0, int64_t m, const int32_t *lab,
+                        hipStream_t s);
+int launch_prune_final(bool gathered, const PruneView &p, int64_t j0,
+                       int64_t m, const int32_t *la, int32_t *lab,
+                       hipStream_t s);
 
 // Sorted sums: counting sort of the sample indices by label (LDS histograms
 // of k bins: k <= SORT_KMAX), then segmented row sums.

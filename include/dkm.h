@@ -152,6 +152,46 @@ int dkm_assign_delta_img_f32(const float *X, const void *image, int64_t n,
                              int32_t *labels, double *delta, int mode,
                              void *stream);
 
+/* Bound-based skipping for the Lloyd loop (Hamerly-style triangle-inequality
+ * bounds; dkm_prune.hip).  Same contract as dkm_assign_delta (labels in/out,
+ * delta +=, identical labels), for the shapes dkm_prune_supported(k, d)
+ * accepts (the single-product screen: d <= 128, d % 8 == 0, k x d within
+ * LDS).  `state` (dkm_prune_state_bytes(n, k, d) bytes, caller-owned) holds
+ * an upper bound on each sample's distance to its label and a lower bound on
+ * its distance to every other centre.  init = 1 screens every sample and
+ * (re)starts the bounds; init = 0 first moves the bounds by how far each
+ * centre moved since the previous call (C_prev = the centres of that call,
+ * k x d fp64) and screens only the samples whose bounds do not prove their
+ * label unchanged, with margins that cover fp64 rounding of the distances.
+ * The state is valid only across consecutive calls on the same X, labels
+ * and a workspace prepared for C.  *n_active (host) receives the number of
+ * samples screened; the call synchronizes `stream` once to read it.  image:
+ * an optional dkm_x_image_* image (used when most samples are screened).
+ * Replaces `_partial_sum`'s assignment (base.py:166-181) for the fit loop. */
+size_t dkm_prune_state_bytes(int64_t n, int64_t k, int64_t d);
+int dkm_prune_supported(int64_t k, int64_t d);
+int dkm_assign_pruned_f64(const double *X, const void *image, int64_t n,
+                          int64_t d, int64_t ldx, const double *C,
+                          const double *C_prev, int64_t k, const void *ws,
+                          size_t ws_bytes, int32_t *labels, double *delta,
+                          void *state, size_t state_bytes, int init,
+                          int64_t *n_active, void *stream);
+int dkm_assign_pruned_f32(const float *X, const void *image, int64_t n,
+                          int64_t d, int64_t ldx, const double *C,
+                          const double *C_prev, int64_t k, const void *ws,
+                          size_t ws_bytes, int32_t *labels, double *delta,
+                          void *state, size_t state_bytes, int init,
+                          int64_t *n_active, void *stream);
+
+/* acc[k*(d+1)] += [sums | counts] of the rows of X by labels (label < 0 or
+ * >= k: skipped): the sums half of dkm_partial_sum for known labels.       */
+int dkm_label_sums_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
+                       const int32_t *labels, int64_t k, const void *ws,
+                       size_t ws_bytes, double *acc, void *stream);
+int dkm_label_sums_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
+                       const int32_t *labels, int64_t k, const void *ws,
+                       size_t ws_bytes, double *acc, void *stream);
+
 /* y[i] += x[i] (device, fp64): acc_new = acc_old + delta.                  */
 int dkm_add_f64(double *y, const double *x, int64_t n, void *stream);
 /* The same, and *nonzero (device int32) <- 1 if any x[i] != 0, else 0:
