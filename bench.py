@@ -182,7 +182,7 @@ def _cpu_task(block, centers, sparse=False):
 # one configuration on the GPU(s)
 # ---------------------------------------------------------------------------
 def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
-               mode, labels, n_blobs=None, f32=False, csr_nnz=0):
+               mode, labels, n_blobs=None, f32=False, csr_nnz=0, host_x=None):
     """One configuration: a fresh fit state, W warmup iterations, then
     exactly K timed iterations (barrier + synchronize on both sides).
     The fit starts at iteration 0 (initial centres, the most expensive
@@ -194,7 +194,12 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
     from dislib_amd.cluster.kmeans import _Lloyd, _init_centers
     from dislib_amd.data import Dataset, Subset
     n_blobs = n_blobs or k
-    if csr_nnz:
+    if host_x is not None:
+        # C1: the reference's own make_blobs (host numpy), rank's slice
+        X = torch.from_numpy(np.ascontiguousarray(
+            host_x[rank * n:(rank + 1) * n])).to(dev)
+        C0 = _init_centers(d, False, k, 0)
+    elif csr_nnz:
         # global rows [rank*n, (rank+1)*n): the ranks shard one dataset
         X = csr_rows(rank * n, n, d, csr_nnz, seed=1)
         C0 = _init_centers(d, True, k, 0).toarray()
@@ -360,6 +365,9 @@ def main():
     sc = a.extras_scale
     extras = [] if a.only_headline else [
         # (name, n, d, k, subset, steps, warmup, fp32 samples, csr nnz/row)
+        ("KMeans k=10 on 100k x 50 fp64 make_blobs per GPU (BASELINE "
+         "configs[0], the reference's CPU-runnable parity case)", 100_000,
+         50, 10, 10_000, 8, 2, False, "c1"),
         ("KMeans k=1000 on 125M x 64 fp64 dense per GPU (BASELINE "
          "configs[2] per-GPU shard; north-star target)",
          125_000_000, 64, 1000, 1_000_000, 8, 2, False, 0),
@@ -386,9 +394,11 @@ def main():
         for i, (_, n, d, k, *_r, f32, nnz) in enumerate(extras):
             if f32:
                 continue          # the fp64 line's baseline covers the shape
-            cpu[i] = cpu_baseline(d, k, a.cpu_seconds / 2,
-                                  _ic(d, bool(nnz), k, 0), k, share,
-                                  csr_nnz=nnz)
+            nz = 0 if nnz == "c1" else nnz
+            cpu[i] = cpu_baseline(d, k, a.cpu_seconds / (4 if nnz == "c1"
+                                                         else 2),
+                                  _ic(d, bool(nz), k, 0), k, share,
+                                  csr_nnz=nz)
 
     import torch
     import torch.distributed as dist
@@ -424,11 +434,17 @@ def main():
                         a.subset, a.steps, a.warmup, a.mode, True)
     ex = []
     for i, (name, n, d, k, sub, steps, warm, f32, nnz) in enumerate(extras):
-        if sc != 1.0:
+        hx = None
+        if nnz == "c1":
+            from sklearn.datasets import make_blobs
+            hx = make_blobs(n_samples=n * world, n_features=d, centers=k,
+                            cluster_std=1.0, random_state=0)[0]
+            nnz = 0
+        elif sc != 1.0:
             n = max(sub, int(n * sc) // sub * sub)
             name += " [scaled to %d rows per GPU]" % n
         rr = run_config(torch, dist, dev, rank, world, n, d, k, sub, steps,
-                        warm, a.mode, False, f32=f32, csr_nnz=nnz)
+                        warm, a.mode, False, f32=f32, csr_nnz=nnz, host_x=hx)
         check_collective(rr)
         e = {"workload": name, "n_per_gpu": n, "d": d, "k": k,
              "dtype": "f32 samples (f64 distances)" if f32 else "f64",

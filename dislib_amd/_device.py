@@ -324,6 +324,13 @@ def add_(y, x, nonzero=None):
                                      stream_ptr()), "dkm_add_f64_nz")
 
 
+def add_dd_(hi, lo, x, nonzero=None):
+    """(hi, lo) += x compensated (hi = the rounded running sums)."""
+    so = _lib.lib()
+    _lib.check(so.dkm_add_f64_dd(ptr(hi), ptr(lo), ptr(x), hi.numel(),
+                                 ptr(nonzero), stream_ptr()), "dkm_add_f64_dd")
+
+
 def predict(dd, C, ws, labels, mode):
     so = _lib.lib()
     k = C.shape[0]

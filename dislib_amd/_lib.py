@@ -64,6 +64,7 @@ SIGNATURES = {
                                   _p, _p]),
     "dkm_add_f64": (_i32, [_p, _p, _i64, _p]),
     "dkm_add_f64_nz": (_i32, [_p, _p, _i64, _p, _p]),
+    "dkm_add_f64_dd": (_i32, [_p, _p, _p, _i64, _p, _p]),
     "dkm_predict_f64": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz, _p,
                                _i32, _p]),
     "dkm_predict_f32": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz, _p,

@@ -140,15 +140,19 @@ class KMeans:
 
 
 # Full recomputation of the running [sums | counts] every REFRESH
-# iterations (1 = every iteration).  Between refreshes the delta updates
-# add rounding of at most REFRESH * 2^-52 * (|S_old| + |moved rows|) per
-# sum element (a shrinking cluster keeps the error of its larger past
-# sums); the fit tests pin the centres at 1e-9 of the oracle with 8.
-# A refresh is skipped when no delta since the last one held a nonzero:
-# then no sample changed cluster, the running sums are bit-identical to
-# that last full recomputation, and they ARE the sums of the current
-# assignment (a converged fit stops re-reading X for them).
-REFRESH = int(os.environ.get("DKM_REFRESH", "8"))
+# iterations (1 = every iteration).  The running state is compensated
+# (dkm_add_f64_dd: hi + lo, TwoSum), so a delta update adds no rounding of
+# the old sums: between refreshes the state differs from a fresh
+# recomputation only by the deltas' own rounding, <= ~2^-52 x (the moved
+# rows' magnitude) per iteration and element -- the error of ONE fresh
+# fp64 sum whenever the rows moved since the refresh weigh no more than the
+# cluster.  With a plain fp64 state every add also rounded |S_old| (the
+# drift grew as REFRESH x 2^-52 |S|), which is what the old 8-iteration
+# refresh bounded; the fit tests pin the centres at 1e-9 of the oracle.
+# A refresh is also skipped when no delta since the last one held a
+# nonzero: then no sample changed cluster and the running sums are
+# bit-identical to that last full recomputation.
+REFRESH = int(os.environ.get("DKM_REFRESH", "64"))
 
 # Bound-based skipping (dkm_assign_pruned_*, dkm_prune.hip): from the second
 # iteration on, samples whose distance bounds prove their label unchanged
@@ -192,6 +196,7 @@ class _Lloyd:
         self.ws = Workspace(k, d, max(1, min(dd.n, 1 << 27)), dd.device)
         self.acc = t.empty(k * (d + 1), dtype=t.float64, device=dd.device)
         self.state = t.zeros(k * (d + 1), dtype=t.float64, device=dd.device)
+        self.state_lo = t.zeros_like(self.state)   # compensation term
         self.diff = t.zeros(k + 1, dtype=t.float64, device=dd.device)
         # [converged, delta nonzero]: read together once per iteration
         self.flag = t.zeros(2, dtype=t.int32, device=dd.device)
@@ -275,16 +280,17 @@ class _Lloyd:
         self.partial()
 
     def reduce_update(self):
-        from .._device import add_, update
+        from .._device import add_dd_, update
         with self._on():
             _shard.allreduce_sum_(self.acc)
             self._was_full = self._full()
             if self._was_full:
                 self.state.copy_(self.acc)
+                self.state_lo.zero_()
             else:
                 # every rank adds the same all-reduced delta: the ranks'
                 # nonzero flags, and so their refresh decisions, agree
-                add_(self.state, self.acc, self.flag[1:])
+                add_dd_(self.state, self.state_lo, self.acc, self.flag[1:])
             update(self.state, self.C, self.sums_mode, self.tol, self.diff,
                    self.flag[:1])
         self.it += 1

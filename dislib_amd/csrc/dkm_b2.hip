@@ -76,11 +76,12 @@ constexpr int B2_SCR_FIXED = 4 * 128 + 1024;
 // entries, own masks.
 constexpr int B2_NLOAD = 4;
 constexpr int B2_S = 3;
-constexpr int B2_CSCR = 4 * 128 + 32 * B2_ENT * 8;
+constexpr int B2_CSCR = 4 * 128 + 32 * B2_ENT * 8 + 128;  // + s_hat_p
 __host__ __device__ constexpr int b2_slot_bytes(int nks) {
   return nks * 1024 + 256;
 }
-static_assert(32 * B2_ENT * 8 <= 1024, "kept entries fit the transpose");
+static_assert(32 * B2_ENT * 8 + 128 <= 1024,
+              "kept entries and s_hat_p fit the transpose");
 
 // v_min3 / v_min without fminf's NaN canonicalisation (inline asm: the
 // compiler would insert v_max_f32 x, x on every MFMA result)
@@ -92,6 +93,27 @@ __device__ __forceinline__ float vmin3(float a, float b, float c) {
 __device__ __forceinline__ float vmin2(float a, float b) {
   float r;
   asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// min of an accumulator's 16 values: one asm statement, so that the
+// compiler pads no hazard nops between the dependent steps (separate asm
+// statements got an s_nop each; plain VALU RAW needs none)
+template <class V16>
+__device__ __forceinline__ float min16(const V16 &a) {
+  float r, t0, t1, t2, t3, t4;
+  asm("v_min3_f32 %1, %6, %7, %8\n\t"
+      "v_min3_f32 %2, %9, %10, %11\n\t"
+      "v_min3_f32 %3, %12, %13, %14\n\t"
+      "v_min3_f32 %4, %15, %16, %17\n\t"
+      "v_min3_f32 %5, %18, %19, %20\n\t"
+      "v_min3_f32 %1, %1, %2, %3\n\t"
+      "v_min3_f32 %4, %4, %5, %21\n\t"
+      "v_min_f32 %0, %1, %4"
+      : "=v"(r), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]),
+        "v"(a[6]), "v"(a[7]), "v"(a[8]), "v"(a[9]), "v"(a[10]), "v"(a[11]),
+        "v"(a[12]), "v"(a[13]), "v"(a[14]), "v"(a[15]));
   return r;
 }
 
@@ -170,6 +192,15 @@ __global__ void __launch_bounds__(SB2)
 
   const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifndef DKM_AB_B2_STAGGER
+#define DKM_AB_B2_STAGGER 0
+#endif
+  // A/B: de-phase the waves sharing a SIMD (waves s, s + 4, s + 8): wave
+  // slot j starts j x DKM_AB_B2_STAGGER x 64 cycles late
+  if (DKM_AB_B2_STAGGER) {
+    for (int t = 0; t < (wid >> 2); ++t)
+      __builtin_amdgcn_s_sleep(DKM_AB_B2_STAGGER);
+  }
   constexpr int NW = PC ? SB2 / 64 - B2_NLOAD : SB2 / 64;  // screening waves
   const int cw = PC ? wid - B2_NLOAD : wid;  // screening wave index
   const int64_t wv = (int64_t)blockIdx.x * NW + cw;
@@ -186,6 +217,10 @@ __global__ void __launch_bounds__(SB2)
   int *s_cnt = (int *)(scr + 256);         // kept entries appended
   float *s_xx = (float *)(scr + 384);      // |x|^2 per sample
   float *s_m = s_xx;                        // M per sample, in process()
+  // s_hat_p per sample, through the block loop (in registers it was one
+  // VGPR too many: a spill reload whose vmcnt(0) waited for the prefetch);
+  // the free tail of the transpose area, past the kept entries
+  float *s_sp = (float *)(scr + 512 + 32 * B2_ENT * 8);
   char *s_tx = scr + 512;                   // one K-step of the tile, bf16
   int2 *s_ent = (int2 *)(scr + 512);       // (score bits, centre), later
   uint32_t *s_om =
@@ -276,7 +311,6 @@ __global__ void __launch_bounds__(SB2)
                      int prv) {
     const int64_t si = s0 + r;
     float xn;
-    const float B2 = bound2_fast(bk, xx, xn);
     const float B2t = bound2_fast(bkt, xx, xn);
     const bool sane0 = (xn < 1e18f) & (xn * cm < 1e30f);
     bool unique = false, two = false, many = false;
@@ -285,10 +319,15 @@ __global__ void __launch_bounds__(SB2)
     bool need3 = true;
     // bounds mode: distance bounds from squared-score bounds, each with a
     // 2^-20 relative margin (the fp32 evaluation, the sqrt, and the
-    // reference's own fp64 rounding); |x|^2 from fp32 within 2^-14
-    float bu = INFINITY, bl1 = -INFINITY, bl0 = -INFINITY;
-    int bi = 0;
-    const float xxh = xx * (1.0f + 0x1.0p-14f), xxl = xx * (1.0f - 0x1.0p-14f);
+    // reference's own fp64 rounding); |x|^2 from fp32 within 2^-14.  Each
+    // path writes its row's bounds where it has them (nothing held live
+    // across the block loop: 6 such VGPRs made the kernel spill, and the
+    // spill reloads' vmcnt waits exposed the prefetched image's latency)
+    const bool bvalid = si < n && h == 0;
+    auto put_bounds = [&](float bu, float bl1, float bl0, int bi) {
+      if (bvalid)
+        v.bnd[si - base] = make_float4(bu, bl1, bl0, __int_as_float(bi));
+    };
     auto ub_of = [](float q2) {
       const float q = __builtin_sqrtf(fmaxf(q2, 0.f));
       return q + q * 0x1.0p-20f;
@@ -304,6 +343,7 @@ __global__ void __launch_bounds__(SB2)
         const int p = pok ? prv : 0;
         // ---- own block: columns = the tile's hinted centres p_c ----------
         f32x16 dn;
+        float dg = 0.f;
         {
           bf16x8 of[NKS];
 #pragma unroll
@@ -317,27 +357,19 @@ __global__ void __launch_bounds__(SB2)
           for (int ks = 0; ks < NKS; ++ks)
             dn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[ks], of[ks], dn, 0,
                                                          0, 0);
-        }
-        // diagonal: row r sits in half (r >> 2) & 1, register
-        // (r & 3) + 4 (r >> 3); the other lane of the pair contributes 0
-        // two-level select (register group r >> 3, then slot r & 3): 15
-        // v_cndmask on 6 lane masks, recomputed per tile (opaque) so that
-        // they are not hoisted into long-lived SGPR pairs
-        float dg;
-        {
-          const int rr = (int)opaque_u32((uint32_t)r);
-          const int q = rr >> 3, w = rr & 3;
-          float sl[4];
+          // s_hat_p's product x_r . (-2 c_p) by VALU dot products: lane
+          // (r, h) holds x_r's and c_p's features 16 ks + 8h .. + 7 (xh and
+          // of), so 4 NKS v_dot2c_f32_bf16 and one cross-half add (exact
+          // bf16 products, an fp32 chain within the bound's chain term).
+          // Selecting the MFMA's diagonal instead (one of 16 registers by a
+          // per-lane index) compiled to ~100 VALU with a hazard nop each.
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            float x = dn[t];
-            x = q == 1 ? dn[4 + t] : x;
-            x = q == 2 ? dn[8 + t] : x;
-            x = q == 3 ? dn[12 + t] : x;
-            sl[t] = x;
-          }
-          dg = w == 0 ? sl[0] : w == 1 ? sl[1] : w == 2 ? sl[2] : sl[3];
-          dg = h == ((rr >> 2) & 1) ? dg : 0.f;
+          for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+            for (int j = 0; j < 8; j += 2)
+              dg = __builtin_amdgcn_fdot2_f32_bf16(
+                  bf16x2{xh[ks][j], xh[ks][j + 1]},
+                  bf16x2{of[ks][j], of[ks][j + 1]}, dg, false);
         }
         {
           float da, db;
@@ -359,6 +391,7 @@ __global__ void __launch_bounds__(SB2)
           s_hp[r] = pok ? p : -1;
           s_cnt[r] = 0;
           s_m[r] = Mr;
+          s_sp[r] = sp;
         }
         for (int w = lane; w < 32 * nkw; w += 64) s_om[w] = 0u;
         wave_sync();
@@ -427,7 +460,10 @@ __global__ void __launch_bounds__(SB2)
             f[ks] = *(const bf16x8 *)(frag + ((int64_t)cb * NKS + ks) * 1024 +
                                       lane * 16);
         };
-        auto rd_n = [&](int cb) { return ncn[cb * 32 + r]; };
+        // (this lane's norm column re-derived per tile: hoisted, it lived
+        // across tiles and was the register the allocator spilled)
+        const float *ncn_r = ncn + (int)opaque_u32((uint32_t)r);
+        auto rd_n = [&](int cb) { return ncn_r[cb * 32]; };
         auto mm = [&](const bf16x8 (&f)[NKS], f32x16 &acc) {
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[0], f[0], cin, 0, 0,
                                                         0);
@@ -447,14 +483,7 @@ __global__ void __launch_bounds__(SB2)
           // 7 v_min3 + 1 v_min on the raw MFMA results (no NaN
           // canonicalisation: a NaN score comes with a NaN threshold, and
           // its sample is rejected by the `sane` test)
-          const float m0 = vmin3(acc[0], acc[1], acc[2]);
-          const float m1 = vmin3(acc[3], acc[4], acc[5]);
-          const float m2 = vmin3(acc[6], acc[7], acc[8]);
-          const float m3 = vmin3(acc[9], acc[10], acc[11]);
-          const float m4 = vmin3(acc[12], acc[13], acc[14]);
-          const float m5 = vmin3(m0, m1, m2);
-          const float m6 = vmin3(m3, m4, acc[15]);
-          any = vmin2(m5, m6) <= thr;
+          any = min16(acc) <= thr;
           if (DKM_AB_B2_PROBE == 2) any = acc[0] == 12345.f;  // (invalid)
         };
         auto append = [&](int cb, const f32x16 &acc, float thr, float nc,
@@ -529,7 +558,10 @@ __global__ void __launch_bounds__(SB2)
         float sv[B2_ENT + 1];
         int cv[B2_ENT + 1];
         bool ok[B2_ENT + 1];
-        sv[0] = sp;
+        // s_hat_p and T again (the same fp32 operation: the same bits)
+        const float sp2 = s_sp[r];
+        const float T2 = pok ? sp2 + B2t : -INFINITY;
+        sv[0] = sp2;
         cv[0] = p;
         ok[0] = true;
 #pragma unroll
@@ -540,7 +572,7 @@ __global__ void __launch_bounds__(SB2)
           // (an index outside [0, k) never reaches the candidate kernels)
           ok[e + 1] = e < cnt && (unsigned)en.y < (unsigned)k;
         }
-        const bool over = cnt > B2_ENT || !pok || !sane0 || !(T < 1e30f);
+        const bool over = cnt > B2_ENT || !pok || !sane0 || !(T2 < 1e30f);
         float bs = INFINITY;
         int bc = 0x7fffffff;
 #pragma unroll
@@ -577,7 +609,7 @@ __global__ void __launch_bounds__(SB2)
           mpk0 = pk[0];
           mpk1 = pk[1];
           mpk2 = pk[2];
-          if (v.bnd && !over) {
+          if (v.bnd) {
             // every centre outside the kept set K = {p} + entries has
             // s_j > s_hat_p + B2t / 2 (+ M unless the row is near); inside
             // K, s_j >= its score - B2t.  The final label is bc unless the
@@ -586,11 +618,16 @@ __global__ void __launch_bounds__(SB2)
 #pragma unroll
             for (int e = 0; e <= B2_ENT; ++e)
               if (ok[e] && !(sv[e] == bs && cv[e] == bc)) m2 = fminf(m2, sv[e]);
-            const float base = sp + 0.25f * B2t + (nearr ? 0.f : 0.99f * Mr);
-            bu = ub_of(xxh + bs + B2t);
-            bl1 = lb_of(xxl + fminf(base, m2 - B2t));
-            bl0 = lb_of(xxl + fminf(base, bs - B2t));
-            bi = bc;
+            const float Mr2 = s_m[r];
+            const float base = sp2 + 0.25f * B2t + (nearr ? 0.f : 0.99f * Mr2);
+            const float xxh = xx * (1.0f + 0x1.0p-14f),
+                        xxl = xx * (1.0f - 0x1.0p-14f);
+            if (over)
+              put_bounds(INFINITY, -INFINITY, -INFINITY, 0);
+            else
+              put_bounds(ub_of(xxh + bs + B2t),
+                         lb_of(xxl + fminf(base, m2 - B2t)),
+                         lb_of(xxl + fminf(base, bs - B2t)), bc);
           }
         }
       }
@@ -697,12 +734,16 @@ __global__ void __launch_bounds__(SB2)
         ins3(o3, j3);
       }
       const bool sane = sane0 & (r1 < 1e30f);
-      if (v.bnd && sane) {
+      const float B2 = bound2_fast(bk, xx, xn);
+      if (v.bnd) {
         // packed scores: within B2 / 2 each (the packing included)
-        bu = ub_of(xxh + r1 + B2);
-        bl1 = lb_of(xxl + r2 - B2);
-        bl0 = lb_of(xxl + r1 - B2);
-        bi = ii1;
+        const float xxh = xx * (1.0f + 0x1.0p-14f),
+                    xxl = xx * (1.0f - 0x1.0p-14f);
+        if (sane)
+          put_bounds(ub_of(xxh + r1 + B2), lb_of(xxl + r2 - B2),
+                     lb_of(xxl + r1 - B2), ii1);
+        else
+          put_bounds(INFINITY, -INFINITY, -INFINITY, 0);
       }
       unique = sane & (r2 - r1 > B2);
       two = sane & !unique & (r3 - r1 > B2);
@@ -710,8 +751,6 @@ __global__ void __launch_bounds__(SB2)
       i2 = ii2;
     }
     const bool valid = si < n && h == 0;
-    if (v.bnd && valid)
-      v.bnd[si - base] = make_float4(bu, bl1, bl0, __int_as_float(bi));
     const int prev = delta ? prv : -1;
     // 3..6 candidates of the threshold pass -> the N-candidate list
     bool nlisted = false;

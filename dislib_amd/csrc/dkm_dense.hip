@@ -2245,6 +2245,29 @@ __global__ void k_add(double *__restrict__ y, const double *__restrict__ x,
   if (nz && __ballot(any) && (threadIdx.x & 63) == 0) nz[0] = 1;
 }
 
+// (hi, lo) += x, compensated: TwoSum of hi + x, the error into lo, then
+// renormalised so that hi = fl(hi + lo) (the running sums the centre update
+// reads) and |lo| <= ulp(hi) / 2.  Built with -ffp-contract=off: every
+// operation rounds on its own, which TwoSum needs.
+__global__ void k_add_dd(double *__restrict__ hi, double *__restrict__ lo,
+                         const double *__restrict__ x, int64_t n, int32_t *nz) {
+  bool any = false;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const double v = x[e];
+    any |= v != 0.0;
+    const double a = hi[e];
+    const double s = a + v;
+    const double bb = s - a;
+    const double err = (a - (s - bb)) + (v - bb);
+    const double t = lo[e] + err;
+    const double h2 = s + t;
+    lo[e] = t - (h2 - s);
+    hi[e] = h2;
+  }
+  if (nz && __ballot(any) && (threadIdx.x & 63) == 0) nz[0] = 1;
+}
+
 // ---------------------------------------------------------------------------
 // host dispatch
 // ---------------------------------------------------------------------------
@@ -3174,6 +3197,19 @@ int dkm_add_f64_nz(double *y, const double *x, int64_t n, int32_t *nonzero,
   const int64_t g = std::min<int64_t>((n + 255) / 256, 4096);
   k_add<<<(unsigned)g, 256, 0, (hipStream_t)stream>>>(y, x, n, nonzero);
   return check_launch("dkm_add_f64_nz");
+}
+
+int dkm_add_f64_dd(double *hi, double *lo, const double *x, int64_t n,
+                   int32_t *nonzero, void *stream) {
+  if ((!hi || !lo || !x) && n > 0) return fail(DKM_E_ARG, "add_dd: NULL");
+  if (nonzero &&
+      hipMemsetAsync(nonzero, 0, 4, (hipStream_t)stream) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "add_dd: flag reset");
+  if (n <= 0) return 0;
+  const int64_t g = std::min<int64_t>((n + 255) / 256, 4096);
+  k_add_dd<<<(unsigned)g, 256, 0, (hipStream_t)stream>>>(hi, lo, x, n,
+                                                          nonzero);
+  return check_launch("dkm_add_f64_dd");
 }
 
 // Result-invalidating A/B timing probes (variants.sh builds only): the

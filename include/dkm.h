@@ -201,6 +201,15 @@ int dkm_add_f64(double *y, const double *x, int64_t n, void *stream);
  * current assignment).                                                   */
 int dkm_add_f64_nz(double *y, const double *x, int64_t n, int32_t *nonzero,
                    void *stream);
+/* The running sums kept compensated: (hi, lo) += x by TwoSum, renormalised
+ * so that hi = fl(hi + lo) -- hi is what dkm_update_centers reads.  Each
+ * add is exact to ~2^-106 |hi|, so the only drift of a delta-updated state
+ * against a fresh recomputation is the rounding of the deltas themselves
+ * (<= ~2^-52 of the moved rows' magnitude per iteration), not the
+ * |sums| x iterations of a plain fp64 add.  nonzero: as dkm_add_f64_nz
+ * (NULL = not wanted).                                                   */
+int dkm_add_f64_dd(double *hi, double *lo, const double *x, int64_t n,
+                   int32_t *nonzero, void *stream);
 
 /* Assignment only.  Replaces `_predict` (base.py:194-201).  Needs a prepared
  * workspace (dkm_prepare_centers with acc = NULL is allowed).             */

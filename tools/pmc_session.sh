@@ -25,6 +25,6 @@ run p3 FETCH_SIZE
 run p3b WRITE_SIZE
 run p4 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_VALU_MFMA_BUSY_CYCLES
 run p5 TA_BUSY_avr TA_TA_BUSY_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum
-python tools/pmc_summary.py $OUT --n $N --traffic-out $OUT/traffic.json \
+python tools/pmc_summary.py $OUT --n $N ${PMC_SUMMARY_ARGS} --traffic-out $OUT/traffic.json \
   > $OUT/summary.txt 2>&1
 echo "== done"
