@@ -87,6 +87,12 @@ def cpu_share():
     return max(1, min(share, aff)), aff
 
 
+def progress(msg):
+    """One line per stage on stderr (long runs: the log keeps growing)."""
+    sys.stderr.write("bench [%s] %s\n" % (time.strftime("%H:%M:%S"), msg))
+    sys.stderr.flush()
+
+
 def cpu_baseline(d, k, target_s, centers, n_blobs, share, csr_nnz=0):
     """One Lloyd iteration's partial sums on a bounded sample of the same
     workload, one Subset per task over a process pool of `share` = (cores,
@@ -95,6 +101,7 @@ def cpu_baseline(d, k, target_s, centers, n_blobs, share, csr_nnz=0):
     by the vectorised oracle.  csr_nnz > 0: CSR rows of the C5 generator
     (the oracle's sklearn-order sparse distances, base.py:169)."""
     cores, machine = share
+    progress("cpu baseline d=%d k=%d nnz=%d" % (d, k, csr_nnz))
     os.environ["OMP_NUM_THREADS"] = "1"        # BLAS threads of the workers
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
     import multiprocessing as mp
@@ -190,6 +197,8 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
     iterations with tol = 0: its wall time (barrier waits excluded) is the
     SURVEY 8(d) whole-loop figure, from the initialised centres through the
     last convergence decision."""
+    progress("gpu n=%d d=%d k=%d steps=%d warmup=%d%s" % (
+        n, d, k, steps, warmup, " csr" if csr_nnz else ""))
     from dislib_amd import _device, _shard
     from dislib_amd.cluster.kmeans import _Lloyd, _init_centers
     from dislib_amd.data import Dataset, Subset

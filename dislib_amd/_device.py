@@ -61,11 +61,10 @@ def ptr(t):
 class DeviceData:
     """HBM image of a Dataset (dense or CSR)."""
 
-    image = None          # the sample image (screen_image)
-
     def __init__(self, dataset, device=None):
         self.device = resolve(device)
-        self._image_failed = False
+        self.images = {}            # sample images by kind (screen_image)
+        self._image_failed = set()
         subsets = list(dataset)
         self.sizes = [int(s.samples.shape[0]) for s in subsets]
         self.offsets = np.concatenate([[0], np.cumsum(self.sizes)]).astype(
@@ -129,31 +128,34 @@ class DeviceData:
     # -- the sample image ---------------------------------------------------
     def screen_image(self, k, mode):
         """The resident bf16 operand image of X (dkm_x_image_*) when the
-        screen that (k, d, mode) selects reads one; built on first use
-        (stream-ordered, one pass over X) and kept with the data, which is
-        immutable.  None when not useful, disabled (DKM_X_IMAGE=0) or when
-        it would leave less than 4 GiB of HBM free."""
+        screen that (k, d, mode) selects reads one, as (tensor, kind);
+        built on first use (stream-ordered, one pass over X) and kept with
+        the data, which is immutable (one image per kind).  (None, 0) when
+        not useful, disabled (DKM_X_IMAGE=0) or when it would leave less
+        than 4 GiB of HBM free."""
         if self.sparse or not X_IMAGE or self.n == 0:
-            return None
-        if self.image is not None:
-            return self.image
+            return None, 0
         so = _lib.lib()
-        if self._image_failed or not so.dkm_x_image_useful(int(k), self.d,
-                                                           int(mode)):
-            return None
+        kind = int(so.dkm_x_image_kind(int(k), self.d, int(mode)))
+        if kind == 0:
+            return None, 0
+        if self.images.get(kind) is not None:
+            return self.images[kind], kind
+        if kind in self._image_failed:
+            return None, 0
         t = torch()
-        nb = int(so.dkm_x_image_bytes(self.n, self.d))
+        nb = int(so.dkm_x_image_bytes(self.n, self.d, kind))
         free = t.cuda.mem_get_info(self.device)[0]
         if nb == 0 or nb + _IMAGE_HEADROOM > free:
-            self._image_failed = True
-            return None
+            self._image_failed.add(kind)
+            return None, 0
         img = t.empty(nb, dtype=t.uint8, device=self.device)
         fn = so.dkm_x_image_f32 if self.dtype == np.float32 else \
             so.dkm_x_image_f64
-        _lib.check(fn(ptr(self.X), self.n, self.d, self.X.stride(0), ptr(img),
-                      nb, stream_ptr()), "dkm_x_image")
-        self.image = img
-        return img
+        _lib.check(fn(ptr(self.X), self.n, self.d, self.X.stride(0), kind,
+                      ptr(img), nb, stream_ptr()), "dkm_x_image")
+        self.images[kind] = img
+        return img, kind
 
     # -- helpers -----------------------------------------------------------
     def subset_slices(self):
@@ -228,11 +230,11 @@ def partial_sum(dd, C, ws, labels, acc, mode):
             ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(acc), stream_ptr()),
             "dkm_partial_sum_csr_f64")
         return
-    img = dd.screen_image(k, mode) if labels is not None else None
+    img, kind = dd.screen_image(k, mode) if labels is not None else (None, 0)
     if img is not None:
         fn = so.dkm_partial_sum_img_f32 if dd.dtype == np.float32 else \
             so.dkm_partial_sum_img_f64
-        _lib.check(fn(ptr(dd.X), ptr(img), dd.n, dd.d, dd.X.stride(0),
+        _lib.check(fn(ptr(dd.X), ptr(img), kind, dd.n, dd.d, dd.X.stride(0),
                       ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(acc), mode,
                       stream_ptr()), "dkm_partial_sum_img")
         return
@@ -253,11 +255,11 @@ def assign_delta(dd, C, ws, labels, delta, mode):
             ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(delta),
             stream_ptr()), "dkm_assign_delta_csr_f64")
         return
-    img = dd.screen_image(k, mode)
+    img, kind = dd.screen_image(k, mode)
     if img is not None:
         fn = so.dkm_assign_delta_img_f32 if dd.dtype == np.float32 else \
             so.dkm_assign_delta_img_f64
-        _lib.check(fn(ptr(dd.X), ptr(img), dd.n, dd.d, dd.X.stride(0),
+        _lib.check(fn(ptr(dd.X), ptr(img), kind, dd.n, dd.d, dd.X.stride(0),
                       ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(delta),
                       mode, stream_ptr()), "dkm_assign_delta_img")
         return
@@ -291,11 +293,12 @@ def assign_pruned(dd, C, C_prev, ws, labels, delta, st):
     samples screened (the others' labels are proven unchanged)."""
     so = _lib.lib()
     k = C.shape[0]
-    img = dd.screen_image(k, _lib.MODE_BF16)
+    img, kind = dd.screen_image(k, _lib.MODE_BF16)
     fn = so.dkm_assign_pruned_f32 if dd.dtype == np.float32 else \
         so.dkm_assign_pruned_f64
     na = ctypes.c_int64(0)
-    _lib.check(fn(ptr(dd.X), ptr(img), dd.n, dd.d, dd.X.stride(0), ptr(C),
+    _lib.check(fn(ptr(dd.X), ptr(img), kind, dd.n, dd.d, dd.X.stride(0),
+                  ptr(C),
                   ptr(C_prev), k, ws.p, ws.nbytes, ptr(labels), ptr(delta),
                   ptr(st.buf), st.nbytes, 0 if st.valid else 1,
                   ctypes.byref(na), stream_ptr()), "dkm_assign_pruned")

@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("DKM_LIB", os.path.join(_HERE, "libdkm.so"))
 # constants mirrored from include/dkm.h
 ABI_VERSION = 1
 MODE_AUTO, MODE_EXACT, MODE_SCREEN32, MODE_BF16X3, MODE_BF16 = 0, 1, 2, 3, 4
+IMAGE_NONE, IMAGE_SINGLE, IMAGE_SPLIT = 0, 1, 2
 SUMS_F64, SUMS_F32, SUMS_RECIP = 0, 1, 2
 PREP_CSR = 1
 COMM_ID_BYTES = 128
@@ -38,25 +39,25 @@ SIGNATURES = {
                                     _p, _p, _i32, _p]),
     "dkm_assign_delta_f32": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz,
                                     _p, _p, _i32, _p]),
-    "dkm_x_image_bytes": (_sz, [_i64, _i64]),
-    "dkm_x_image_useful": (_i32, [_i64, _i64, _i32]),
-    "dkm_x_image_f64": (_i32, [_p, _i64, _i64, _i64, _p, _sz, _p]),
-    "dkm_x_image_f32": (_i32, [_p, _i64, _i64, _i64, _p, _sz, _p]),
-    "dkm_partial_sum_img_f64": (_i32, [_p, _p, _i64, _i64, _i64, _p, _i64,
-                                       _p, _sz, _p, _p, _i32, _p]),
-    "dkm_partial_sum_img_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _i64,
-                                       _p, _sz, _p, _p, _i32, _p]),
-    "dkm_assign_delta_img_f64": (_i32, [_p, _p, _i64, _i64, _i64, _p, _i64,
-                                        _p, _sz, _p, _p, _i32, _p]),
-    "dkm_assign_delta_img_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _i64,
-                                        _p, _sz, _p, _p, _i32, _p]),
+    "dkm_x_image_kind": (_i32, [_i64, _i64, _i32]),
+    "dkm_x_image_bytes": (_sz, [_i64, _i64, _i32]),
+    "dkm_x_image_f64": (_i32, [_p, _i64, _i64, _i64, _i32, _p, _sz, _p]),
+    "dkm_x_image_f32": (_i32, [_p, _i64, _i64, _i64, _i32, _p, _sz, _p]),
+    "dkm_partial_sum_img_f64": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p,
+                                       _i64, _p, _sz, _p, _p, _i32, _p]),
+    "dkm_partial_sum_img_f32": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p,
+                                       _i64, _p, _sz, _p, _p, _i32, _p]),
+    "dkm_assign_delta_img_f64": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p,
+                                        _i64, _p, _sz, _p, _p, _i32, _p]),
+    "dkm_assign_delta_img_f32": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p,
+                                        _i64, _p, _sz, _p, _p, _i32, _p]),
     "dkm_prune_state_bytes": (_sz, [_i64, _i64, _i64]),
     "dkm_prune_supported": (_i32, [_i64, _i64]),
-    "dkm_assign_pruned_f64": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, _i64,
-                                     _p, _sz, _p, _p, _p, _sz, _i32,
+    "dkm_assign_pruned_f64": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p, _p,
+                                     _i64, _p, _sz, _p, _p, _p, _sz, _i32,
                                      ctypes.POINTER(_i64), _p]),
-    "dkm_assign_pruned_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, _i64,
-                                     _p, _sz, _p, _p, _p, _sz, _i32,
+    "dkm_assign_pruned_f32": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p, _p,
+                                     _i64, _p, _sz, _p, _p, _p, _sz, _i32,
                                      ctypes.POINTER(_i64), _p]),
     "dkm_label_sums_f64": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz,
                                   _p, _p]),

@@ -1030,25 +1030,29 @@ static bool b2pc_enabled() {
 }
 
 // ---- the sample image (dkm_x_image_*) ----------------------------------
-size_t x_image_bytes(int64_t n, int64_t d) {
-  const int64_t nt = (n + 31) / 32;
-  return (size_t)nt * (dpad16(d) / 16) * 1024 + (size_t)nt * 128;
+static int64_t img_tile_bytes(int64_t d, int kind) {
+  return kind == IMG_SPLIT ? 4096 : (dpad16(d) / 16) * 1024;
 }
 
-XImage x_image_view(const void *image, int64_t n, int64_t d) {
+size_t x_image_bytes(int64_t n, int64_t d, int kind) {
+  const int64_t nt = (n + 31) / 32;
+  return (size_t)nt * img_tile_bytes(d, kind) + (size_t)nt * 128;
+}
+
+XImage x_image_view(const void *image, int64_t n, int64_t d, int kind) {
   XImage im;
   im.tiles = (const uint16_t *)image;
   im.xx = (const float *)((const char *)image +
-                          (size_t)((n + 31) / 32) * (dpad16(d) / 16) * 1024);
+                          (size_t)((n + 31) / 32) * img_tile_bytes(d, kind));
+  im.kind = kind;
   return im;
 }
 
 // One workgroup per 32-row tile (grid-stride): the tile's rows are read
 // with consecutive lanes on consecutive features (whole lines), staged as
-// fp32 in LDS, then written in operand order -- lane l of K-step ks holds
-// row l & 31, features 16 ks + 8 (l >> 5) .. + 7 -- with the same
-// fp64 -> fp32 -> bf16 roundings the converting screen applies.  |x|^2 is
-// summed in fp64 over the fp32 values and rounded once.
+// fp32 in LDS, then written in operand order with the same fp64 -> fp32 ->
+// bf16 roundings the converting screens apply.  |x|^2 is summed in fp64
+// over the fp32 values and rounded once.
 template <class TX, int NKS>
 __global__ void __launch_bounds__(256)
     k_x_image(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
@@ -1090,17 +1094,70 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// IMG_SPLIT (d <= 32): hi and lo parts in k_screen_w32's B-operand order
 template <class TX>
-int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, void *image,
-                   int cus, hipStream_t s) {
-  const int nks = (int)(dpad16(d) / 16);
-  const XImage im = x_image_view(image, n, d);
+__global__ void __launch_bounds__(256)
+    k_x_image_split(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
+                    uint16_t *__restrict__ tiles, float *__restrict__ xx) {
+  constexpr int LD = 33;
+  __shared__ float s[32 * LD];
+  const int64_t nt = (n + 31) / 32;
+  for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int64_t r0 = t * 32;
+    __syncthreads();
+    for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+      const int row = e >> 5, col = e & 31;
+      float v = 0.f;
+      if (r0 + row < n && col < d) v = (float)X[(r0 + row) * ldx + col];
+      s[row * LD + col] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      double a = 0.0;
+      for (int c = 0; c < 32; ++c) {
+        const double v = s[threadIdx.x * LD + c];
+        a = fma(v, v, a);
+      }
+      xx[r0 + threadIdx.x] = (float)a;
+    }
+    {
+      const int e = threadIdx.x;  // 256 = 4 blocks x 64 lanes
+      const int blk = e >> 6, l = e & 63, ks = blk & 1, lo = blk >> 1;
+      const float *src = s + (l & 31) * LD + 16 * (l >> 5) + 8 * ks;
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const bf16x2 h2 = __builtin_convertvector(f32x2{src[j], src[j + 1]},
+                                                  bf16x2);
+        const uint32_t hu = __builtin_bit_cast(uint32_t, h2);
+        const bf16x2 l2 = __builtin_convertvector(
+            f32x2{src[j] - __uint_as_float(hu << 16),
+                  src[j + 1] - __uint_as_float(hu & 0xffff0000u)},
+            bf16x2);
+        o[j] = lo ? l2[0] : h2[0];
+        o[j + 1] = lo ? l2[1] : h2[1];
+      }
+      *((bf16x8 *)(tiles + t * 2048) + e) = o;
+    }
+  }
+}
+
+template <class TX>
+int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, int kind,
+                   void *image, int cus, hipStream_t s) {
+  const XImage im = x_image_view(image, n, d, kind);
   const int64_t nt = (n + 31) / 32;
   const unsigned g =
       (unsigned)std::max<int64_t>(1, std::min<int64_t>(nt, (int64_t)cus * 8));
   uint16_t *tiles = (uint16_t *)image;
   float *xx = (float *)im.xx;
-  switch (nks) {
+  if (kind == IMG_SPLIT) {
+    if (d > 32) return fail(DKM_E_ARG, "x_image: split image needs d <= 32");
+    k_x_image_split<TX><<<g, 256, 0, s>>>(X, n, d, ldx, tiles, xx);
+    return check_launch("sample image (split)");
+  }
+  if (kind != IMG_SINGLE) return fail(DKM_E_ARG, "x_image: bad kind");
+  switch ((int)(dpad16(d) / 16)) {
 #define DKM_XI(N)                                                         \
   case N:                                                                 \
     k_x_image<TX, N><<<g, 256, 0, s>>>(X, n, d, ldx, tiles, xx);          \
@@ -1115,8 +1172,8 @@ int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, void *image,
 }
 
 template int launch_x_image<double>(const double *, int64_t, int, int64_t,
-                                    void *, int, hipStream_t);
-template int launch_x_image<float>(const float *, int64_t, int, int64_t,
+                                    int, void *, int, hipStream_t);
+template int launch_x_image<float>(const float *, int64_t, int, int64_t, int,
                                    void *, int, hipStream_t);
 
 template <class TX>
@@ -1129,8 +1186,8 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
   const size_t lds = pc ? b2pc_lds_bytes(k, d) : b2_lds_bytes(k, d);
   if (lds > 160 * 1024) return 1;  // caller uses k_screen_b1
   // the image path reads whole tiles: the range must start on one
-  const bool im = img.tiles && !pc && base % 32 == 0;
-  if (!im) img = XImage{nullptr, nullptr};
+  const bool im = img.tiles && img.kind == IMG_SINGLE && !pc && base % 32 == 0;
+  if (!im) img = XImage{nullptr, nullptr, IMG_NONE};
   const int nks = (int)(dpad16(d) / 16);
   const bool w1 = kpad32(k) <= 1024;
   const void *kf = nullptr;

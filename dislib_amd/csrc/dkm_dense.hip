@@ -960,12 +960,12 @@ __device__ __forceinline__ void wave_sync_w() {
 #ifndef DKM_W32_WPE
 #define DKM_W32_WPE 3
 #endif
-template <class TX>
+template <class TX, bool IMG>
 __global__ void __launch_bounds__(SBW) __attribute__((
     amdgpu_waves_per_eu(DKM_W32_WPE)))
     k_screen_w32(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
                  int k, WsView v, int32_t *__restrict__ lab_out, double *acc,
-                 int amode, int64_t base, int use_list) {
+                 int amode, int64_t base, int use_list, XImage img) {
   constexpr int GB = 8;  // 32-centre blocks per packing group
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int nkb = (int)(kpad32(k) / 32);
@@ -1059,10 +1059,47 @@ __global__ void __launch_bounds__(SBW) __attribute__((
     return 32 * row + 16 * (q ^ ((row >> 3) & 1));
   };
 
+  // IMG (IMG_SPLIT image, delta / labels-only launches): the tile's hi and
+  // lo slices and |x|^2 come ready in operand order, 4 whole-line 16-B
+  // loads per lane, the next tile's in flight while this one is scored
+  bf16x8 qi[4];
+  float qxx = 0.f;
+  int qpv = -1;
+  auto load_img = [&](int64_t s0) {
+    const bf16x8 *src =
+        (const bf16x8 *)(img.tiles + (s0 >> 5) * 2048) + lane;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) qi[q] = __builtin_nontemporal_load(src + 64 * q);
+    qxx = __builtin_nontemporal_load(img.xx + s0 + r);
+    if (delta) {
+      const int64_t rows = std::max<int64_t>(0, n - s0);
+      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(lab_out + std::min(s0, n)), 0,
+          (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
+      qpv = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
+    }
+  };
   int64_t s0 = base + wv * 32;
-  if (s0 < n) load_tile(s0);
+  if (s0 < n) {
+    if constexpr (IMG)
+      load_img(s0);
+    else
+      load_tile(s0);
+  }
   for (; s0 < n; s0 += step) {
     bf16x8 xh[2], xl[2];
+    float xx;
+    int prv;
+    const int64_t s_next = s0 + step;
+    if constexpr (IMG) {
+      xh[0] = qi[0];
+      xh[1] = qi[1];
+      xl[0] = qi[2];
+      xl[1] = qi[3];
+      xx = qxx;
+      prv = qpv;
+      if (s_next < n) load_img(s_next);
+    } else {
     float xp[IC];
 #pragma unroll
     for (int i = 0; i < IC; ++i) xp[i] = 0.f;
@@ -1115,10 +1152,10 @@ __global__ void __launch_bounds__(SBW) __attribute__((
       if (lpos == 0) s_xx[RI * i + lrow] = xp[i];
     }
     wave_sync_w();
-    const float xx = s_xx[r];
-    const int prv = pv;
-    const int64_t s_next = s0 + step;
+    xx = s_xx[r];
+    prv = pv;
     if (!full_acc && s_next < n) load_tile(s_next);
+    }  // !IMG
 
     float r1 = INFINITY, r2 = INFINITY;
     int ri = 0;
@@ -1200,7 +1237,7 @@ __global__ void __launch_bounds__(SBW) __attribute__((
     } else {
       tl_over += add;
     }
-    if (full_acc) {
+    if (!IMG && full_acc) {
       // the loading lanes add their pieces of the decided rows
       if (h == 0) s_lab[r] = si < n && unique ? ri : -1;
       wave_sync_w();
@@ -1247,7 +1284,7 @@ __global__ void __launch_bounds__(SBW) __attribute__((
         }
       }
     }
-    if (full_acc && s_next < n) load_tile(s_next);
+    if (!IMG && full_acc && s_next < n) load_tile(s_next);
   }
   if (lane == 0) {
     if (listing) v.tcount[seg] = tl_cnt;
@@ -2366,16 +2403,26 @@ template <class TX>
 static int launch_screen_w32(const TX *X, int64_t end, int d, int64_t ldx,
                              int k, const WsView &v, int32_t *lab_out,
                              double *acc, int amode, int64_t base, size_t lds,
-                             int use_list, hipStream_t s, int *nseg) {
-  const void *kf = (const void *)k_screen_w32<TX>;
+                             int use_list, hipStream_t s, int *nseg,
+                             XImage img) {
+  // the image serves launches that need no sums from the raw rows
+  const bool im = img.tiles && img.kind == IMG_SPLIT && !am_full(amode) &&
+                  base % 32 == 0;
+  const void *kf = im ? (const void *)k_screen_w32<TX, true>
+                      : (const void *)k_screen_w32<TX, false>;
   lds += (size_t)(SBW / 64) * W32_SCR;  // the waves' transpose scratch
   const int64_t cap = (int64_t)dev_info().cus * resident_blocks(kf, SBW, lds);
   const int64_t per_block = 32 * (SBW / 64);
   const int64_t need = (end - base + per_block - 1) / per_block;
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min(need, cap));
   *nseg = (int)std::min<int64_t>((int64_t)g * (SBW / 64), TL_SEGS);
-  k_screen_w32<TX><<<g, SBW, lds, s>>>(X, end, d, ldx, k, v, lab_out, acc,
-                                      amode, base, use_list);
+  if (im)
+    k_screen_w32<TX, true><<<g, SBW, lds, s>>>(X, end, d, ldx, k, v, lab_out,
+                                               acc, amode, base, use_list, img);
+  else
+    k_screen_w32<TX, false><<<g, SBW, lds, s>>>(
+        X, end, d, ldx, k, v, lab_out, acc, amode, base, use_list,
+        XImage{nullptr, nullptr, IMG_NONE});
   return check_launch("screen assignment (32x32)");
 }
 
@@ -2786,7 +2833,7 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                                            nseg, s);
     } else if (w32)
       r = launch_screen_w32<TX>(X, end, d, ldx, k, v, lab_out, acc, amode,
-                                base, lds, use_list, s, &nseg);
+                                base, lds, use_list, s, &nseg, img);
     else if (prec == P_F32)
       r = vec ? launch_screen_nks<P_F32, true, TX>(X, end, d, ldx, k, v,
                                                    lab_out, acc, amode, base,
@@ -2858,7 +2905,8 @@ template <class TX>
 static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                   const double *C, int64_t k, const void *ws, size_t wsb,
                   int32_t *labels, double *acc, int acc_kind, int mode,
-                  void *stream, const char *who, const void *image = nullptr) {
+                  void *stream, const char *who, const void *image = nullptr,
+                  int image_kind = 0) {
   if (n < 0 || d <= 0 || k <= 0 || ldx < d)
     return fail(DKM_E_ARG, std::string(who) + ": bad n/d/k/ldx");
   if (d > INT32_MAX || k > INT32_MAX)
@@ -2896,8 +2944,8 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
     const int prec = mode == DKM_MODE_SCREEN32 ? P_F32
                      : mode == DKM_MODE_SCREEN_BF16 ? P_B1
                                                     : P_B3;
-    const XImage img = image ? x_image_view(image, n, d)
-                             : XImage{nullptr, nullptr};
+    const XImage img = image ? x_image_view(image, n, d, image_kind)
+                             : XImage{nullptr, nullptr, IMG_NONE};
     return launch_screen<TX>(prec, X, n, (int)d, ldx, C, (int)k, v, wsb,
                              labels, acc, acc_kind, s, img);
   }
@@ -2905,7 +2953,7 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
 }
 
 template <class TX>
-static int x_image(const TX *X, int64_t n, int64_t d, int64_t ldx,
+static int x_image(const TX *X, int64_t n, int64_t d, int64_t ldx, int kind,
                    void *image, size_t image_bytes, void *stream,
                    const char *who) {
   if (n < 0 || d <= 0 || ldx < d)
@@ -2913,9 +2961,11 @@ static int x_image(const TX *X, int64_t n, int64_t d, int64_t ldx,
   if (d > 128) return fail(DKM_E_ARG, std::string(who) + ": d > 128");
   if (n == 0) return 0;
   if (!X || !image) return fail(DKM_E_ARG, std::string(who) + ": NULL");
-  if (image_bytes < x_image_bytes(n, d))
+  if (kind != IMG_SINGLE && kind != IMG_SPLIT)
+    return fail(DKM_E_ARG, std::string(who) + ": bad image kind");
+  if (image_bytes < x_image_bytes(n, d, kind))
     return fail(DKM_E_WORKSPACE, std::string(who) + ": image too small");
-  return launch_x_image<TX>(X, n, (int)d, ldx, image, dev_info().cus,
+  return launch_x_image<TX>(X, n, (int)d, ldx, kind, image, dev_info().cus,
                             (hipStream_t)stream);
 }
 
@@ -2927,7 +2977,8 @@ static bool prune_ok(int64_t k, int64_t d) {
 }
 
 template <class TX>
-static int assign_pruned(const TX *X, const void *image, int64_t n, int64_t d,
+static int assign_pruned(const TX *X, const void *image, int image_kind,
+                         int64_t n, int64_t d,
                          int64_t ldx, const double *C, const double *Cp,
                          int64_t k, const void *ws, size_t wsb,
                          int32_t *labels, double *delta, void *state,
@@ -2966,14 +3017,15 @@ static int assign_pruned(const TX *X, const void *image, int64_t n, int64_t d,
   const bool gather = !init && na * 5 <= n * 2;
   const int64_t total = gather ? na : n;
   const int nks = (int)(dpad16(d) / 16);
-  const XImage img0 =
-      image ? x_image_view(image, n, d) : XImage{nullptr, nullptr};
+  const XImage img0 = image && image_kind == IMG_SINGLE
+                         ? x_image_view(image, n, d, IMG_SINGLE)
+                         : XImage{nullptr, nullptr, IMG_NONE};
   for (int64_t j0 = 0; j0 < total; j0 += cap) {
     const int64_t m = std::min(cap, total - j0);
     const TX *Xc;
     int64_t ldc;
     int32_t *lc;
-    XImage img{nullptr, nullptr};
+    XImage img{nullptr, nullptr, IMG_NONE};
     if (gather) {
       if (int r = launch_prune_gather<TX>(X, ldx, (int)d, p, j0, m, labels, s))
         return r;
@@ -2985,7 +3037,8 @@ static int assign_pruned(const TX *X, const void *image, int64_t n, int64_t d,
       ldc = ldx;
       lc = labels + j0;
       if (img0.tiles)
-        img = XImage{img0.tiles + (j0 / 32) * nks * 512, img0.xx + j0};
+        img = XImage{img0.tiles + (j0 / 32) * nks * 512, img0.xx + j0,
+                     IMG_SINGLE};
     }
     if (int r = launch_screen<TX>(P_B1, Xc, m, (int)d, ldc, C, (int)k, v, wsb,
                                   lc, delta, 2, s, img, p.bnd))
@@ -3069,52 +3122,69 @@ int dkm_predict_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
                        mode, stream, "dkm_predict_f32");
 }
 
-int dkm_x_image_useful(int64_t k, int64_t d, int mode) {
-  if (k <= 0 || d <= 0 || d > 128 || k > INT32_MAX) return 0;
-  if (gemm_path(k, d) || !screen_ok(k, d) || !b1_ok(k, d)) return 0;
-  const bool single = mode == DKM_MODE_SCREEN_BF16 ||
-                      (mode == DKM_MODE_AUTO && !sums_fit_lds(k, d));
-  return single && b2_enabled() && b2_lds_bytes(k, d) <= 160 * 1024 ? 1 : 0;
+int dkm_x_image_kind(int64_t k, int64_t d, int mode) {
+  if (k <= 0 || d <= 0 || d > 128 || k > INT32_MAX) return IMG_NONE;
+  if (gemm_path(k, d) || !screen_ok(k, d)) return IMG_NONE;
+  if (mode == DKM_MODE_AUTO)
+    mode = b1_ok(k, d) && !sums_fit_lds(k, d) ? DKM_MODE_SCREEN_BF16
+                                              : DKM_MODE_SCREEN_BF16X3;
+  if (mode == DKM_MODE_SCREEN_BF16)
+    return b1_ok(k, d) && b2_enabled() && b2_lds_bytes(k, d) <= 160 * 1024
+               ? IMG_SINGLE
+               : IMG_NONE;
+  if (mode == DKM_MODE_SCREEN_BF16X3)
+    return d <= 32 && (size_t)(kpad32(k) / 32) * (4096 + 128) <= LDS_BUDGET &&
+                   !AB_NO_W32
+               ? IMG_SPLIT
+               : IMG_NONE;
+  return IMG_NONE;
 }
 
-size_t dkm_x_image_bytes(int64_t n, int64_t d) {
+size_t dkm_x_image_bytes(int64_t n, int64_t d, int kind) {
   if (n < 0 || d <= 0 || d > 128) return 0;
-  return x_image_bytes(n, d);
+  if (kind == IMG_SPLIT && d > 32) return 0;
+  if (kind != IMG_SINGLE && kind != IMG_SPLIT) return 0;
+  return x_image_bytes(n, d, kind);
 }
 
 int dkm_x_image_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
-                    void *image, size_t image_bytes, void *stream) {
-  return x_image<double>(X, n, d, ldx, image, image_bytes, stream,
+                    int kind, void *image, size_t image_bytes, void *stream) {
+  return x_image<double>(X, n, d, ldx, kind, image, image_bytes, stream,
                          "dkm_x_image_f64");
 }
 
 int dkm_x_image_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
-                    void *image, size_t image_bytes, void *stream) {
-  return x_image<float>(X, n, d, ldx, image, image_bytes, stream,
+                    int kind, void *image, size_t image_bytes, void *stream) {
+  return x_image<float>(X, n, d, ldx, kind, image, image_bytes, stream,
                         "dkm_x_image_f32");
 }
 
-int dkm_partial_sum_img_f64(const double *X, const void *image, int64_t n,
+int dkm_partial_sum_img_f64(const double *X, const void *image, int image_kind,
+                             int64_t n,
                             int64_t d, int64_t ldx, const double *C,
                             int64_t k, const void *ws, size_t ws_bytes,
                             int32_t *labels, double *acc, int mode,
                             void *stream) {
   if (!acc) return fail(DKM_E_ARG, "partial_sum: acc is NULL");
   return assign<double>(X, n, d, ldx, C, k, ws, ws_bytes, labels, acc, 1,
-                        mode, stream, "dkm_partial_sum_img_f64", image);
+                        mode, stream, "dkm_partial_sum_img_f64", image,
+                        image_kind);
 }
 
-int dkm_partial_sum_img_f32(const float *X, const void *image, int64_t n,
+int dkm_partial_sum_img_f32(const float *X, const void *image, int image_kind,
+                             int64_t n,
                             int64_t d, int64_t ldx, const double *C,
                             int64_t k, const void *ws, size_t ws_bytes,
                             int32_t *labels, double *acc, int mode,
                             void *stream) {
   if (!acc) return fail(DKM_E_ARG, "partial_sum: acc is NULL");
   return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, acc, 1,
-                       mode, stream, "dkm_partial_sum_img_f32", image);
+                       mode, stream, "dkm_partial_sum_img_f32", image,
+                        image_kind);
 }
 
-int dkm_assign_delta_img_f64(const double *X, const void *image, int64_t n,
+int dkm_assign_delta_img_f64(const double *X, const void *image, int image_kind,
+                              int64_t n,
                              int64_t d, int64_t ldx, const double *C,
                              int64_t k, const void *ws, size_t ws_bytes,
                              int32_t *labels, double *delta, int mode,
@@ -3122,10 +3192,12 @@ int dkm_assign_delta_img_f64(const double *X, const void *image, int64_t n,
   if (!labels || !delta)
     return fail(DKM_E_ARG, "assign_delta: labels and delta are required");
   return assign<double>(X, n, d, ldx, C, k, ws, ws_bytes, labels, delta, 2,
-                        mode, stream, "dkm_assign_delta_img_f64", image);
+                        mode, stream, "dkm_assign_delta_img_f64", image,
+                        image_kind);
 }
 
-int dkm_assign_delta_img_f32(const float *X, const void *image, int64_t n,
+int dkm_assign_delta_img_f32(const float *X, const void *image, int image_kind,
+                              int64_t n,
                              int64_t d, int64_t ldx, const double *C,
                              int64_t k, const void *ws, size_t ws_bytes,
                              int32_t *labels, double *delta, int mode,
@@ -3133,7 +3205,8 @@ int dkm_assign_delta_img_f32(const float *X, const void *image, int64_t n,
   if (!labels || !delta)
     return fail(DKM_E_ARG, "assign_delta: labels and delta are required");
   return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, delta, 2,
-                       mode, stream, "dkm_assign_delta_img_f32", image);
+                       mode, stream, "dkm_assign_delta_img_f32", image,
+                        image_kind);
 }
 
 size_t dkm_prune_state_bytes(int64_t n, int64_t k, int64_t d) {
@@ -3143,24 +3216,28 @@ size_t dkm_prune_state_bytes(int64_t n, int64_t k, int64_t d) {
 
 int dkm_prune_supported(int64_t k, int64_t d) { return prune_ok(k, d) ? 1 : 0; }
 
-int dkm_assign_pruned_f64(const double *X, const void *image, int64_t n,
+int dkm_assign_pruned_f64(const double *X, const void *image, int image_kind,
+                           int64_t n,
                           int64_t d, int64_t ldx, const double *C,
                           const double *C_prev, int64_t k, const void *ws,
                           size_t ws_bytes, int32_t *labels, double *delta,
                           void *state, size_t state_bytes, int init,
                           int64_t *n_active, void *stream) {
-  return assign_pruned<double>(X, image, n, d, ldx, C, C_prev, k, ws, ws_bytes,
+  return assign_pruned<double>(X, image, image_kind, n, d, ldx, C, C_prev, k,
+                               ws, ws_bytes,
                                labels, delta, state, state_bytes, init,
                                n_active, stream, "dkm_assign_pruned_f64");
 }
 
-int dkm_assign_pruned_f32(const float *X, const void *image, int64_t n,
+int dkm_assign_pruned_f32(const float *X, const void *image, int image_kind,
+                           int64_t n,
                           int64_t d, int64_t ldx, const double *C,
                           const double *C_prev, int64_t k, const void *ws,
                           size_t ws_bytes, int32_t *labels, double *delta,
                           void *state, size_t state_bytes, int init,
                           int64_t *n_active, void *stream) {
-  return assign_pruned<float>(X, image, n, d, ldx, C, C_prev, k, ws, ws_bytes,
+  return assign_pruned<float>(X, image, image_kind, n, d, ldx, C, C_prev, k,
+                              ws, ws_bytes,
                               labels, delta, state, state_bytes, init,
                               n_active, stream, "dkm_assign_pruned_f32");
 }

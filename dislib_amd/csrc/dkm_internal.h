@@ -147,19 +147,25 @@ struct WsView {
 bool b2_enabled();
 int b2_probe();  // != 0: a result-invalidating timing probe build
 size_t b2_lds_bytes(int64_t k, int64_t d);
-// The sample image (dkm_x_image_*): X's rows as bf16 MFMA A operands,
-// 32-row tiles of dpad16(d) / 16 K-steps x 1 KB, then fp32 |x|^2 per row
-// (rows and features past n, d zero).  With one, k_screen_b2 streams
-// 2 B per feature instead of sizeof(TX) and skips the conversion.
+// The sample image (dkm_x_image_*): a resident bf16 copy of X in the
+// operand order of the screen that reads it, then fp32 |x|^2 per row
+// (rows and features past n, d zero).  Kinds:
+//  IMG_SINGLE (k_screen_b2): 32-row tiles of dpad16(d) / 16 K-steps x 1 KB,
+//    lane l of K-step s = row l & 31, features 16 s + 8 (l >> 5) .. + 7;
+//  IMG_SPLIT (k_screen_w32, d <= 32): 32-row tiles of 4 x 1 KB (hi K-slice
+//    0, hi 1, lo 0, lo 1), lane l of slice s = row l & 31, features
+//    16 (l >> 5) + 8 s .. + 7, hi = bf16(fl32(x)), lo = bf16(fl32(x) - hi).
+constexpr int IMG_NONE = 0, IMG_SINGLE = 1, IMG_SPLIT = 2;
 struct XImage {
   const uint16_t *tiles;
   const float *xx;
+  int kind;
 };
-size_t x_image_bytes(int64_t n, int64_t d);
-XImage x_image_view(const void *image, int64_t n, int64_t d);
+size_t x_image_bytes(int64_t n, int64_t d, int kind);
+XImage x_image_view(const void *image, int64_t n, int64_t d, int kind);
 template <class TX>
-int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, void *image,
-                   int cus, hipStream_t s);
+int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, int kind,
+                   void *image, int cus, hipStream_t s);
 template <class TX>
 int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
                      const WsView &v, int32_t *lab_out, int64_t base,

@@ -112,45 +112,52 @@ int dkm_assign_delta_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
                          size_t ws_bytes, int32_t *labels, double *delta,
                          int mode, void *stream);
 
-/* The sample image: a resident bf16 copy of X (rows rounded fp64 -> fp32
- * -> bf16, laid out as the screen's MFMA operands in 32-row tiles) plus
- * fp32 |x|^2 per row; dkm_x_image_bytes(n, d) bytes (0: d > 128).  Built
- * once per dataset (it depends only on X), it lets the label-hinted
- * threshold screen (MODE_SCREEN_BF16 with d <= 128) stream 2 B per feature
- * instead of 8: labels, sums and re-checks still come from X itself, so
- * results are identical with or without it.  An image is valid only for the
- * exact X, n and d it was built from; rebuild it if X changes.  The _img
- * forms of dkm_partial_sum / dkm_assign_delta take it (NULL = none); every
- * other argument is theirs.  Same interface as base.py:166-181.            */
-size_t dkm_x_image_bytes(int64_t n, int64_t d);
-/* 1 when the screen that (k, d, mode) selects reads a sample image (the
- * label-hinted single-product screen, MODE_SCREEN_BF16 or the AUTO choice
- * for sums beyond LDS), else 0: building one would be wasted.            */
-int dkm_x_image_useful(int64_t k, int64_t d, int mode);
+/* The sample image: a resident bf16 copy of X in the operand order of the
+ * screen that reads it, plus fp32 |x|^2 per row.  Built once per dataset
+ * (it depends only on X): the screen then streams 2 or 4 B per feature
+ * instead of sizeof(X) and skips the conversion.  Labels, sums and
+ * re-checks still come from X itself, so results are identical with or
+ * without it.  An image is valid only for the exact X, n and d (and kind)
+ * it was built from; rebuild it if X changes.
+ *   kind DKM_IMAGE_SINGLE: bf16(fl32(x)) for the label-hinted
+ *     single-product screen (MODE_SCREEN_BF16 or the AUTO choice when the
+ *     sums exceed LDS; d <= 128);
+ *   kind DKM_IMAGE_SPLIT: bf16 hi and lo of fl32(x) for the d <= 32
+ *     bf16x3 screen (MODE_SCREEN_BF16X3 or the AUTO choice), read by its
+ *     delta / labels-only launches.
+ * dkm_x_image_kind(k, d, mode) says which kind the selected screen reads
+ * (DKM_IMAGE_NONE: building one would be wasted).  The _img forms of
+ * dkm_partial_sum / dkm_assign_delta take it (image NULL = none); every
+ * other argument is theirs.  Same interface as base.py:166-181.          */
+#define DKM_IMAGE_NONE 0
+#define DKM_IMAGE_SINGLE 1
+#define DKM_IMAGE_SPLIT 2
+int dkm_x_image_kind(int64_t k, int64_t d, int mode);
+size_t dkm_x_image_bytes(int64_t n, int64_t d, int kind);
 int dkm_x_image_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
-                    void *image, size_t image_bytes, void *stream);
+                    int kind, void *image, size_t image_bytes, void *stream);
 int dkm_x_image_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
-                    void *image, size_t image_bytes, void *stream);
-int dkm_partial_sum_img_f64(const double *X, const void *image, int64_t n,
-                            int64_t d, int64_t ldx, const double *C,
-                            int64_t k, const void *ws, size_t ws_bytes,
-                            int32_t *labels, double *acc, int mode,
-                            void *stream);
-int dkm_partial_sum_img_f32(const float *X, const void *image, int64_t n,
-                            int64_t d, int64_t ldx, const double *C,
-                            int64_t k, const void *ws, size_t ws_bytes,
-                            int32_t *labels, double *acc, int mode,
-                            void *stream);
-int dkm_assign_delta_img_f64(const double *X, const void *image, int64_t n,
-                             int64_t d, int64_t ldx, const double *C,
-                             int64_t k, const void *ws, size_t ws_bytes,
-                             int32_t *labels, double *delta, int mode,
-                             void *stream);
-int dkm_assign_delta_img_f32(const float *X, const void *image, int64_t n,
-                             int64_t d, int64_t ldx, const double *C,
-                             int64_t k, const void *ws, size_t ws_bytes,
-                             int32_t *labels, double *delta, int mode,
-                             void *stream);
+                    int kind, void *image, size_t image_bytes, void *stream);
+int dkm_partial_sum_img_f64(const double *X, const void *image, int image_kind,
+                            int64_t n, int64_t d, int64_t ldx,
+                            const double *C, int64_t k, const void *ws,
+                            size_t ws_bytes, int32_t *labels, double *acc,
+                            int mode, void *stream);
+int dkm_partial_sum_img_f32(const float *X, const void *image, int image_kind,
+                            int64_t n, int64_t d, int64_t ldx,
+                            const double *C, int64_t k, const void *ws,
+                            size_t ws_bytes, int32_t *labels, double *acc,
+                            int mode, void *stream);
+int dkm_assign_delta_img_f64(const double *X, const void *image,
+                             int image_kind, int64_t n, int64_t d,
+                             int64_t ldx, const double *C, int64_t k,
+                             const void *ws, size_t ws_bytes, int32_t *labels,
+                             double *delta, int mode, void *stream);
+int dkm_assign_delta_img_f32(const float *X, const void *image, int image_kind,
+                             int64_t n, int64_t d, int64_t ldx,
+                             const double *C, int64_t k, const void *ws,
+                             size_t ws_bytes, int32_t *labels, double *delta,
+                             int mode, void *stream);
 
 /* Bound-based skipping for the Lloyd loop (Hamerly-style triangle-inequality
  * bounds; dkm_prune.hip).  Same contract as dkm_assign_delta (labels in/out,
@@ -166,18 +173,18 @@ int dkm_assign_delta_img_f32(const float *X, const void *image, int64_t n,
  * The state is valid only across consecutive calls on the same X, labels
  * and a workspace prepared for C.  *n_active (host) receives the number of
  * samples screened; the call synchronizes `stream` once to read it.  image:
- * an optional dkm_x_image_* image (used when most samples are screened).
+ * an optional DKM_IMAGE_SINGLE image (used when most samples are screened).
  * Replaces `_partial_sum`'s assignment (base.py:166-181) for the fit loop. */
 size_t dkm_prune_state_bytes(int64_t n, int64_t k, int64_t d);
 int dkm_prune_supported(int64_t k, int64_t d);
-int dkm_assign_pruned_f64(const double *X, const void *image, int64_t n,
-                          int64_t d, int64_t ldx, const double *C,
+int dkm_assign_pruned_f64(const double *X, const void *image, int image_kind,
+                          int64_t n, int64_t d, int64_t ldx, const double *C,
                           const double *C_prev, int64_t k, const void *ws,
                           size_t ws_bytes, int32_t *labels, double *delta,
                           void *state, size_t state_bytes, int init,
                           int64_t *n_active, void *stream);
-int dkm_assign_pruned_f32(const float *X, const void *image, int64_t n,
-                          int64_t d, int64_t ldx, const double *C,
+int dkm_assign_pruned_f32(const float *X, const void *image, int image_kind,
+                          int64_t n, int64_t d, int64_t ldx, const double *C,
                           const double *C_prev, int64_t k, const void *ws,
                           size_t ws_bytes, int32_t *labels, double *delta,
                           void *state, size_t state_bytes, int init,

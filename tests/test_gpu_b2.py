@@ -214,12 +214,13 @@ def test_sample_image_layout(n, d):
     rng = np.random.default_rng(n + d)
     x = rng.standard_normal((n, d)) * 10.0 ** rng.integers(-3, 4, (n, 1))
     X = torch.from_numpy(x).cuda()
-    nb = so.dkm_x_image_bytes(n, d)
+    nb = so.dkm_x_image_bytes(n, d, _lib.IMAGE_SINGLE)
     nt, nks = (n + 31) // 32, (d + 15) // 16
     assert nb == nt * nks * 1024 + nt * 128
     img = torch.zeros(nb, dtype=torch.uint8, device="cuda")
-    _lib.check(so.dkm_x_image_f64(_device.ptr(X), n, d, d, _device.ptr(img),
-                                  nb, _device.stream_ptr()), "image")
+    _lib.check(so.dkm_x_image_f64(_device.ptr(X), n, d, d, _lib.IMAGE_SINGLE,
+                                  _device.ptr(img), nb, _device.stream_ptr()),
+               "image")
     raw = img.cpu().numpy()
     tiles = raw[:nt * nks * 1024].view(np.uint16).reshape(nt, nks, 64, 8)
     xx = raw[nt * nks * 1024:].view(np.float32)

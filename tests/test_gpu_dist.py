@@ -17,6 +17,7 @@ import sys
 
 import numpy as np
 import pytest
+from scipy.sparse import csr_matrix
 
 from oracle import kmeans_oracle as orc
 
@@ -103,7 +104,9 @@ def test_world2_fit_predict_vs_oracle(case, tmp_path):
     ref = orc.OracleKMeans(n_clusters=k, max_iter=iters, tol=tol,
                            random_state=0)
     real_init = orc.init_centers
-    orc.init_centers = lambda *a: r0["init"].copy()
+    # (the reference wraps sparse initial centres in a CSR matrix)
+    orc.init_centers = lambda d_, sparse, *a: (
+        csr_matrix(r0["init"]) if sparse else r0["init"].copy())
     try:
         rl = ref.fit(blocks, sparse=case == "csr", set_labels=True)
     finally:

@@ -40,7 +40,7 @@ class _Pruned:
         self.ws = _device.Workspace(k, self.d, self.dd.n, self.dev)
         self.st = _device.PruneState(self.dd, k)
         if not image:
-            self.dd._image_failed = True
+            self.dd._image_failed = {1, 2}
         self.lab = torch.full((self.dd.n,), -1, dtype=torch.int32,
                               device=self.dev)
         self.Cp = torch.zeros((k, self.d), dtype=torch.float64,
