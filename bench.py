@@ -68,8 +68,9 @@ def parse():
     p.add_argument("--backend", default="nccl",
                    help="process-group backend for N > 1 (nccl = RCCL; gloo "
                         "only to rehearse several ranks on one GPU)")
-    p.add_argument("--traffic-json", default=os.path.join(
-        ROOT, "profiles", "r02_traffic.json"))
+    p.add_argument("--traffic-json", default=None,
+                   help="PMC traffic summary for the headline (default: "
+                        "profiles/traffic/d<d>_k<k>.json when present)")
     return p.parse_args()
 
 
@@ -273,12 +274,32 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
            if world > 1 else "none",
            "rccl_ranks": info[0] if info else None,
            "pruned": st.pstate is not None,
+           # the sample image the screen streamed (dkm_x_image_*), if any
+           "image_kind": max(st.dd.images) if getattr(st.dd, "images", None)
+           else 0,
            # samples screened per pruned iteration (whole fit; the first is
            # the bounds' initial full pass)
            "active": list(st.active)}
     del st, ds, X
     torch.cuda.empty_cache()
     return out
+
+
+def traffic_for(n, d, k, path=None):
+    """HBM bytes per assignment call from the committed PMC passes
+    (tools/pmc_session.sh -> tools/pmc_summary.py --traffic-out): the
+    per-sample read + write bytes of the screen and re-check kernels,
+    scaled to n; None when no summary for this (d, k) is committed."""
+    path = path or os.path.join(ROOT, "profiles", "traffic",
+                                "d%d_k%d.json" % (d, k))
+    try:
+        tj = json.load(open(path))
+        if tj.get("d") == d and tj.get("k") == k:
+            return n * (tj["hbm_read_bytes_per_sample"] +
+                        tj["hbm_write_bytes_per_sample"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
 
 
 def prune_fields(r, n):
@@ -333,6 +354,16 @@ def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
                              "frac": g / sec / 1e12 / L2_PEAK_TBS}}
     elif d <= 128:
         b = n * (8 * d + 8)
+        ik = r.get("image_kind", 0)
+        # bytes the screen actually streams per sample: the resident bf16
+        # image (SPLIT: hi + lo, 4 KB per 32-row tile; SINGLE: 1 KB per
+        # 16-feature K-step per tile) + fp32 |x|^2, or X itself; + labels
+        if ik == 2:
+            sb = 4096 // 32 + 4 + 8
+        elif ik == 1:
+            sb = (d + 15) // 16 * 1024 // 32 + 4 + 8
+        else:
+            sb = es * d + 8
         out = {"bound": "hbm", "achieved": b / sec / 1e9,
                "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": b / sec / 1e9 / HBM_PEAK_GBS,
@@ -346,7 +377,14 @@ def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
                "mfma_products": screen_products(k, d),
                "mfma_bf16_tflops_executed":
                    2.0 * screen_products(k, d) * k * d * n / sec / 1e12,
-               "mfma_bf16_peak_tflops": BF16_PEAK_TFLOPS}
+               "mfma_bf16_peak_tflops": BF16_PEAK_TFLOPS,
+               "image": {0: "none (X converted in the screen)",
+                         1: "bf16 single (resident, built in the fit)",
+                         2: "bf16 hi+lo split (resident, built in the "
+                            "fit)"}[ik],
+               "streamed_bytes_per_sample": sb,
+               "streamed_gbs": n * sb / sec / 1e9,
+               "streamed_frac": n * sb / sec / 1e9 / HBM_PEAK_GBS}
     else:
         # auto mode runs the single-product GEMM screen (bf16 hi x hi on
         # hi-only tiles, features padded to 64)
@@ -460,8 +498,10 @@ def main():
              "value": n * world * steps / rr["el"],
              "unit": "samples·iters/s", "ms_per_step": rr["el"] / steps * 1e3,
              "steps": steps, "warmup": warm,
-             "roofline": roofline(n, d, k, rr, False, 4 if f32 else 8,
-                                  csr_nnz=nnz),
+             "roofline": dict(roofline(n, d, k, rr, False, 4 if f32 else 8,
+                                       csr_nnz=nnz),
+                              traffic=None if f32 or nnz else
+                              traffic_for(n, d, k)),
              "rechecked_samples": rr["rechecked"],
              "pruning": prune_fields(rr, n)}
         e.update(fit_fields(rr, n, world))
@@ -471,9 +511,15 @@ def main():
             e["predict_samples_per_s"] = n / (rr["pred_ms"] * 1e-3)
         if world > 1:
             e["rccl_ranks"] = rr["rccl_ranks"]
-        if i in cpu:
-            cpu[i]["gpu_over_cpu"] = e["value"] / cpu[i]["value"]
-            e["cpu_baseline"] = cpu[i]
+        ci = i if i in cpu else (i - 1 if f32 and (i - 1) in cpu else None)
+        if ci is not None:
+            cb = dict(cpu[ci])
+            if ci != i:     # fp32 samples: the same fp64-distance arithmetic
+                cb["note"] = ("the fp64 line's measurement: the reference's "
+                              "fp32 path computes the same fp64 distances "
+                              "(base.py:204-205 on fp32 rows upcast)")
+            cb["gpu_over_cpu"] = e["value"] / cb["value"]
+            e["cpu_baseline"] = cb
         ex.append(e)
 
     if rank != 0:
@@ -485,16 +531,7 @@ def main():
 
     value = a.n * world * a.steps / r["el"]
     rf = roofline(a.n, a.d, a.k, r, a.labels)
-    if os.path.exists(a.traffic_json):
-        # HBM bytes per launch from the committed PMC passes
-        # (tools/pmc_session.sh -> tools/pmc_summary.py --traffic-out)
-        try:
-            tj = json.load(open(a.traffic_json))
-            if tj.get("d") == a.d and tj.get("k") == a.k:
-                rf["traffic"] = a.n * (tj["hbm_read_bytes_per_sample"] +
-                                       tj["hbm_write_bytes_per_sample"])
-        except (OSError, ValueError, KeyError):
-            pass
+    rf["traffic"] = traffic_for(a.n, a.d, a.k, a.traffic_json)
     out = {
         "metric": METRIC,
         "value": value,

@@ -17,6 +17,9 @@
 //                  entered only by lanes whose r beats their K-th).
 //     k_knn_merge  lane = query: the P partial lists merged by (r, index),
 //                  sqrt, int64 indices.
+//   n_neighbors > 32: passes of up to 32 columns; pass c starts strictly
+//   after the (r, index) where pass c - 1 ended (a per-query floor), so the
+//   passes enumerate the same (r, index) order, 32 entries at a time.
 //   Roofline: VALU fp64 -- 3 d ops (sub, mul, add) per pair.
 //
 // * Epsilon query: DBSCAN _compute_neighbours (reference
@@ -117,7 +120,8 @@ __global__ void __launch_bounds__(NB)
     k_knn_part(const double *__restrict__ Q, int64_t nq, int64_t ldq,
                const double *__restrict__ X, int64_t nx, int64_t ldx, int d,
                int64_t plen, int P, double *__restrict__ pr,
-               int *__restrict__ pi) {
+               int *__restrict__ pi, const double *__restrict__ flr,
+               const int *__restrict__ fli) {
   const int lane = threadIdx.x & 63;
   const int64_t qg = (int64_t)blockIdx.x * (NB / 64) +
                      __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -136,9 +140,19 @@ __global__ void __launch_bounds__(NB)
   const int64_t j0 = (int64_t)p * plen;
   const int64_t j1 = std::min<int64_t>(nx, j0 + plen);
   cdouble *xc = (cdouble *)X;
-  for (int64_t j = j0; j < j1; ++j) {
-    const double r = seq_r<MAXD>(qv, qrow, xc + j * ldx, d);
-    top.push_seq(r, (int)j);
+  if (flr) {
+    // a later pass: only (r, j) strictly after the previous pass's last
+    const double fr = live ? flr[q] : INFINITY;
+    const int fi = live ? fli[q] : INT32_MAX;
+    for (int64_t j = j0; j < j1; ++j) {
+      const double r = seq_r<MAXD>(qv, qrow, xc + j * ldx, d);
+      if (r > fr || (r == fr && (int)j > fi)) top.push_seq(r, (int)j);
+    }
+  } else {
+    for (int64_t j = j0; j < j1; ++j) {
+      const double r = seq_r<MAXD>(qv, qrow, xc + j * ldx, d);
+      top.push_seq(r, (int)j);
+    }
   }
   if (!live) return;
   double *po = pr + (q * P + p) * K;
@@ -154,7 +168,8 @@ template <int K>
 __global__ void __launch_bounds__(NB)
     k_knn_merge(const double *__restrict__ pr, const int *__restrict__ pi,
                 int64_t nq, int P, int kn, double *__restrict__ out_d,
-                int64_t *__restrict__ out_i) {
+                int64_t *__restrict__ out_i, int64_t ldo,
+                double *__restrict__ flr, int *__restrict__ fli) {
   const int64_t q = (int64_t)blockIdx.x * NB + threadIdx.x;
   if (q >= nq) return;
   TopK<K> top;
@@ -172,8 +187,12 @@ __global__ void __launch_bounds__(NB)
 #pragma unroll
   for (int s = 0; s < K; ++s)
     if (s < kn) {
-      out_d[q * kn + s] = sqrt(top.r[s]);
-      out_i[q * kn + s] = (int64_t)top.i[s];
+      out_d[q * ldo + s] = sqrt(top.r[s]);
+      out_i[q * ldo + s] = (int64_t)top.i[s];
+      if (s == kn - 1) {  // where the next pass starts
+        flr[q] = top.r[s];
+        fli[q] = top.i[s];
+      }
     }
 }
 
@@ -393,21 +412,23 @@ void knn_grid(int64_t nq, int64_t nx, int64_t *plen, int *P) {
 template <int MAXD, int K>
 void launch_knn_part(dim3 g, hipStream_t s, const double *Q, int64_t nq,
                      int64_t ldq, const double *X, int64_t nx, int64_t ldx,
-                     int d, int64_t plen, int P, double *pr, int *pi) {
+                     int d, int64_t plen, int P, double *pr, int *pi,
+                     const double *flr, const int *fli) {
   k_knn_part<MAXD, K><<<g, NB, 0, s>>>(Q, nq, ldq, X, nx, ldx, d, plen, P, pr,
-                                       pi);
+                                       pi, flr, fli);
 }
 
 template <int K>
 int knn_dispatch(int maxd, dim3 g, hipStream_t s, const double *Q, int64_t nq,
                  int64_t ldq, const double *X, int64_t nx, int64_t ldx, int d,
-                 int64_t plen, int P, double *pr, int *pi) {
+                 int64_t plen, int P, double *pr, int *pi, const double *flr,
+                 const int *fli) {
   switch (maxd) {
-    case 8: launch_knn_part<8, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi); break;
-    case 16: launch_knn_part<16, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi); break;
-    case 32: launch_knn_part<32, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi); break;
-    case 64: launch_knn_part<64, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi); break;
-    default: launch_knn_part<0, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi); break;
+    case 8: launch_knn_part<8, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi, flr, fli); break;
+    case 16: launch_knn_part<16, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi, flr, fli); break;
+    case 32: launch_knn_part<32, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi, flr, fli); break;
+    case 64: launch_knn_part<64, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi, flr, fli); break;
+    default: launch_knn_part<0, K>(g, s, Q, nq, ldq, X, nx, ldx, d, plen, P, pr, pi, flr, fli); break;
   }
   return check_launch("knn partial lists");
 }
@@ -416,8 +437,8 @@ int knn_args(const double *Q, int64_t nq, int64_t ldq, const double *X,
              int64_t nx, int64_t ldx, int64_t d, int64_t kn) {
   if (nq < 0 || nx < 1 || d < 1 || ldq < d || ldx < d)
     return fail(DKM_E_ARG, "knn: bad nq/nx/d/ld");
-  if (kn < 1 || kn > 32 || kn > nx)
-    return fail(DKM_E_ARG, "knn: n_neighbors must be in [1, min(32, nx)]");
+  if (kn < 1 || kn > nx)
+    return fail(DKM_E_ARG, "knn: n_neighbors must be in [1, nx]");
   if (nx > INT32_MAX || d > INT32_MAX)
     return fail(DKM_E_ARG, "knn: nx/d too large");
   if (nq > 0 && (!Q || !X)) return fail(DKM_E_ARG, "knn: NULL Q/X");
@@ -469,12 +490,14 @@ using namespace dkm;
 extern "C" {
 
 size_t dkm_knn_workspace_bytes(int64_t nq, int64_t nx, int64_t kn) {
-  if (nq < 0 || nx < 1 || kn < 1 || kn > 32) return 0;
+  if (nq < 0 || nx < 1 || kn < 1 || kn > nx) return 0;
   int64_t plen;
   int P;
   knn_grid(std::max<int64_t>(nq, 1), nx, &plen, &P);
-  const int K = knn_k(kn);
-  return (size_t)std::max<int64_t>(nq, 1) * P * K * (8 + 4) + 256;
+  const int K = knn_k(std::min<int64_t>(kn, 32));
+  const int64_t q = std::max<int64_t>(nq, 1);
+  // partial lists of one pass, then the per-query floor (r, index)
+  return (size_t)q * P * K * (8 + 4) + (size_t)q * (8 + 4) + 512;
 }
 
 int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
@@ -492,31 +515,43 @@ int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
   int64_t plen;
   int P;
   knn_grid(nq, nx, &plen, &P);
-  const int K = knn_k(kn);
+  const int KP = knn_k(std::min<int64_t>(kn, 32));
   double *pr = (double *)ws;
-  int *pi = (int *)(pr + (size_t)nq * P * K);
+  int *pi = (int *)(pr + (size_t)nq * P * KP);
+  double *flr = (double *)(((uintptr_t)(pi + (size_t)nq * P * KP) + 255) &
+                           ~(uintptr_t)255);
+  int *fli = (int *)(flr + nq);
   const dim3 g((unsigned)((nq + 255) / 256), (unsigned)P);
   const int maxd = maxd_of(d);
-  int r;
-  switch (K) {
-    case 1: r = knn_dispatch<1>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
-    case 2: r = knn_dispatch<2>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
-    case 4: r = knn_dispatch<4>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
-    case 8: r = knn_dispatch<8>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
-    case 16: r = knn_dispatch<16>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
-    default: r = knn_dispatch<32>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi); break;
-  }
-  if (r) return r;
   const unsigned gm = (unsigned)((nq + NB - 1) / NB);
-  switch (K) {
-    case 1: k_knn_merge<1><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
-    case 2: k_knn_merge<2><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
-    case 4: k_knn_merge<4><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
-    case 8: k_knn_merge<8><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
-    case 16: k_knn_merge<16><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
-    default: k_knn_merge<32><<<gm, NB, 0, s>>>(pr, pi, nq, P, (int)kn, out_dist, out_idx); break;
+  for (int64_t c0 = 0; c0 < kn; c0 += 32) {
+    const int kk = (int)std::min<int64_t>(32, kn - c0);
+    const int K = knn_k(kk);
+    const double *fr = c0 ? flr : nullptr;
+    const int *fi = c0 ? fli : nullptr;
+    int r;
+    switch (K) {
+      case 1: r = knn_dispatch<1>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi, fr, fi); break;
+      case 2: r = knn_dispatch<2>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi, fr, fi); break;
+      case 4: r = knn_dispatch<4>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi, fr, fi); break;
+      case 8: r = knn_dispatch<8>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi, fr, fi); break;
+      case 16: r = knn_dispatch<16>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi, fr, fi); break;
+      default: r = knn_dispatch<32>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi, fr, fi); break;
+    }
+    if (r) return r;
+    double *od = out_dist + c0;
+    int64_t *oi = out_idx + c0;
+    switch (K) {
+      case 1: k_knn_merge<1><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
+      case 2: k_knn_merge<2><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
+      case 4: k_knn_merge<4><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
+      case 8: k_knn_merge<8><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
+      case 16: k_knn_merge<16><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
+      default: k_knn_merge<32><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
+    }
+    if (int e = check_launch("knn merge")) return e;
   }
-  return check_launch("knn merge");
+  return 0;
 }
 
 int dkm_radius_count_f64(const double *Q, int64_t nq, int64_t ldq,

@@ -16,7 +16,9 @@ order reproduces; the distances here are the exactly ordered ones
 Differences from the reference (documented, not reproduced):
 * ``_merge_queries`` walks ``range(n_samples)`` with the *fit* Subset size
   (``base.py:96``); the rows are the query rows here.
-* ``n_neighbors`` is at most 32 (the kernel's register-resident top-k).
+* ``n_neighbors`` beyond 32 runs in passes of 32 columns (the kernel's
+  register-resident top-k), each starting after the previous pass's last
+  (distance, index).
 * Sparse Subsets are not supported on this path.
 """
 import ctypes
@@ -39,7 +41,6 @@ class NearestNeighbors:
         GPU to run on (default: the current device).
     """
 
-    MAX_NEIGHBORS = 32
 
     def __init__(self, n_neighbors=5, *, device=None):
         self._n_neighbors = n_neighbors
@@ -113,8 +114,5 @@ def _check_n_neighbors(n_neighbors, fit_dataset):
             raise ValueError(
                 "Expected n_neighbors <= n_samples_fit, but n_neighbors = %d,"
                 " n_samples_fit = %d" % (n_neighbors, n_fit))
-    if n_neighbors > NearestNeighbors.MAX_NEIGHBORS:
-        raise ValueError("dislib_amd NearestNeighbors: n_neighbors <= %d"
-                         % NearestNeighbors.MAX_NEIGHBORS)
     if len(fit_dataset) == 0:
         raise ValueError("NearestNeighbors: the fitted Dataset is empty")

@@ -32,6 +32,8 @@ KNN_CASES = [
     ("kn_half", 120, None, 4, 30, 16, "uniform"),    # k >= n_fit // 2: brute
     ("kn_other", 200, 100, 6, 50, 4, "blobs"),       # queries != fit data
     ("kn_one", 90, None, 2, 30, 1, "uniform"),       # single neighbour
+    ("kn_40", 400, None, 3, 100, 40, "blobs"),       # > 32: two passes
+    ("kn_70", 300, None, 4, 100, 70, "uniform"),     # > 64, brute regime
 ]
 # (name, n, d, subset, epsilon, min_samples, begin, end)
 DB_CASES = [

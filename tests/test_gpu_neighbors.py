@@ -61,6 +61,9 @@ def test_kneighbors_reference_golden(name):
     (700, 3000, 70, 8, 2),       # d > 64: query read from memory
     (129, 300, 64, 1, 3),        # ragged last wave, one neighbour
     (64, 257, 9, 17, 4),         # k between templates (K = 32 slots)
+    (500, 3000, 5, 33, 5),       # n_neighbors > 32: a second pass of one
+    (300, 2000, 12, 100, 6),     # four passes, the last of 4 columns
+    (200, 700, 70, 64, 7),       # exactly two full passes, d > 64
 ])
 def test_kneighbors_vs_oracle(nq, nx, d, kn, seed):
     rng = np.random.default_rng(seed)

@@ -54,6 +54,8 @@ def main():
             v = vals[a.skip:] if len(vals) > a.skip else vals
             row[c] = sum(x[1] for x in v) / len(v)
             row["_launches"] = len(v)
+            # only steady-state launches count towards the traffic figure
+            row["_steady"] = len(vals) > a.skip
         if "FETCH_SIZE" in row:
             row["hbm_read_bytes"] = 2 * row["FETCH_SIZE"] * 1024
         if "WRITE_SIZE" in row:
@@ -65,7 +67,9 @@ def main():
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)
     if a.traffic_out:
-        ks = [k for k in out if k.startswith(("k_screen", "k_recheck"))]
+        ks = [k for k in out
+              if k.startswith(("k_screen", "k_recheck", "k_cand"))
+              and out[k].get("_steady")]
         rd = sum(out[k].get("hbm_read_bytes", 0.0) for k in ks)
         wr = sum(out[k].get("hbm_write_bytes", 0.0) for k in ks)
         json.dump({"kernels": ks, "n": a.n, "d": a.d, "k": a.k,
