@@ -17,6 +17,7 @@ import re
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     m = re.match(r"(?:void )?(?:dkm::)?([A-Za-z_0-9]+)", name)
     return m.group(1) if m else name[:30]
 
@@ -30,6 +31,43 @@ def load(d):
                 (int(r["Dispatch_Id"]), float(r["Counter_Value"]),
                  int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     return per
+
+
+ASSIGN = ("k_screen", "k_recheck", "k_cand", "k_gemm")
+
+
+def last_iteration_bytes(d):
+    """Read / write HBM bytes of the assignment kernels dispatched in the
+    last complete iteration (the window between the last two k_criterion
+    dispatches) of the FETCH_SIZE / WRITE_SIZE passes."""
+    tot = {}
+    kset = set()
+    for ctr, scale in (("FETCH_SIZE", 2 * 1024), ("WRITE_SIZE", 1024)):
+        rows = []
+        for f in sorted(glob.glob(os.path.join(d, "*",
+                                               "run_counter_collection.csv"))):
+            for r in csv.DictReader(open(f)):
+                if r["Counter_Name"] == ctr or (
+                        r["Kernel_Name"].find("k_criterion") >= 0 and
+                        r["Counter_Name"] == ctr):
+                    rows.append(r)
+        if not rows:
+            return None, None, None
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        crit = [int(r["Dispatch_Id"]) for r in rows
+                if "k_criterion" in r["Kernel_Name"]]
+        if len(crit) < 2:
+            return None, None, None
+        lo, hi = crit[-2], crit[-1]
+        t = 0.0
+        for r in rows:
+            did = int(r["Dispatch_Id"])
+            k = short(r["Kernel_Name"])
+            if lo < did < hi and k.startswith(ASSIGN):
+                t += float(r["Counter_Value"]) * scale
+                kset.add(k)
+        tot[ctr] = t
+    return tot["FETCH_SIZE"], tot["WRITE_SIZE"], sorted(kset)
 
 
 def main():
@@ -67,8 +105,23 @@ def main():
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)
     if a.traffic_out:
+        it_rd, it_wr, it_ks = last_iteration_bytes(a.dir)
+        if it_rd is not None:
+            json.dump({"kernels": it_ks, "n": a.n, "d": a.d, "k": a.k,
+                       "hbm_read_bytes_per_sample": it_rd / a.n,
+                       "hbm_write_bytes_per_sample": it_wr / a.n,
+                       "source": os.path.abspath(a.dir).split("/repo/")[-1],
+                       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                 "passes, KiB; reads x2 (gfx950 FETCH_SIZE "
+                                 "= 1/2 of a wide streaming read, "
+                                 "MI355X_MICROARCH.md HBM); the assignment "
+                                 "kernels of the last whole iteration "
+                                 "(between the last two k_criterion "
+                                 "dispatches), every launch of it"},
+                      open(a.traffic_out, "w"), indent=1)
+            return
         ks = [k for k in out
-              if k.startswith(("k_screen", "k_recheck", "k_cand"))
+              if k.startswith(("k_screen", "k_recheck", "k_cand", "k_gemm"))
               and out[k].get("_steady")]
         rd = sum(out[k].get("hbm_read_bytes", 0.0) for k in ks)
         wr = sum(out[k].get("hbm_write_bytes", 0.0) for k in ks)
