@@ -14,7 +14,13 @@ Here the concatenated samples are uploaded once and ``dkm_radius_count_f64``
 k-means exact arithmetic), select ``dist < epsilon``, and sort each list by
 (distance, index).  The reference's ``np.argsort`` gives the same order
 except among exactly equal distances, which it may order differently.
-Dense Subsets only.
+
+Sparse Subsets (``sparse=True``, the reference's ``pairwise_distances``
+branch, ``:130``) go through ``dkm_radius_count_csr_f64`` /
+``dkm_radius_fill_csr_f64``: sklearn 1.7's fp64 CSR expansion
+``sqrt(max(-2 q.x + |q|^2 + |x|^2, 0))`` in its own operation order.  The
+concatenated CSR matrix is taken with sorted column indices (a sorted copy
+when a Subset's are not; scipy's products then follow the same order).
 """
 import ctypes
 
@@ -29,8 +35,8 @@ def compute_neighbours(epsilon, min_samples, sparse, begin_idx, end_idx,
     """Same arguments and results as the reference task: a list of int64
     index arrays (one per query sample) and a list of core-point flags."""
     if sparse:
-        raise ValueError("compute_neighbours: sparse Subsets are not "
-                         "supported by the GPU path")
+        return _compute_neighbours_csr(epsilon, min_samples, begin_idx,
+                                       end_idx, subsets, device)
     t = torch()
     dev = resolve(device)
     with on(dev):
@@ -62,6 +68,70 @@ def compute_neighbours(epsilon, min_samples, sparse, begin_idx, end_idx,
     neigh = [idx[offsets[i]:offsets[i + 1]] for i in range(nq)]
     core = [bool(c[i] >= min_samples) for i in range(nq)]
     return neigh, core
+
+
+def _compute_neighbours_csr(epsilon, min_samples, begin_idx, end_idx,
+                            subsets, device):
+    t = torch()
+    dev = resolve(device)
+    m = _concat_csr(subsets)
+    n, d = m.shape
+    b, e = _slice_bounds(begin_idx, end_idx, n)
+    nq = e - b
+    if nq == 0:
+        return [], []
+    so = _lib.lib()
+    with on(dev):
+        indptr = t.from_numpy(m.indptr.astype(np.int64)).to(dev)
+        indices = t.from_numpy(
+            np.ascontiguousarray(m.indices, dtype=np.int32)).to(dev)
+        data = t.from_numpy(
+            np.ascontiguousarray(m.data, dtype=np.float64)).to(dev)
+        if data.numel() == 0:  # keep valid device pointers
+            indices = t.zeros(1, dtype=t.int32, device=dev)
+            data = t.zeros(1, dtype=t.float64, device=dev)
+        counts = t.empty(nq, dtype=t.int64, device=dev)
+        _lib.check(so.dkm_radius_count_csr_f64(
+            ptr(indptr), ptr(indices), ptr(data), n, d, b, nq,
+            float(epsilon), ptr(counts), stream_ptr()), "dkm_radius_count_csr")
+        c = counts.cpu().numpy()
+        offsets = np.concatenate([[0], np.cumsum(c)]).astype(np.int64)
+        total = int(offsets[-1])
+        off_d = t.from_numpy(offsets).to(dev)
+        out_i = t.empty(max(total, 1), dtype=t.int64, device=dev)
+        out_d = t.empty(max(total, 1), dtype=t.float64, device=dev)
+        wsb = int(so.dkm_radius_workspace_bytes(nq, total))
+        ws = t.empty(wsb, dtype=t.uint8, device=dev)
+        _lib.check(so.dkm_radius_fill_csr_f64(
+            ptr(indptr), ptr(indices), ptr(data), n, d, b, nq,
+            float(epsilon), ptr(off_d), ctypes.c_void_p(ws.data_ptr()), wsb,
+            ptr(out_i), ptr(out_d), stream_ptr()), "dkm_radius_fill_csr")
+        idx = out_i[:total].cpu().numpy()
+    neigh = [idx[offsets[i]:offsets[i + 1]] for i in range(nq)]
+    core = [bool(c[i] >= min_samples) for i in range(nq)]
+    return neigh, core
+
+
+def _concat_csr(subsets):
+    """The concatenated sparse samples as one CSR matrix with sorted column
+    indices (``_concatenate_subsets`` -> ``vstack``, classes.py:144-150)."""
+    import scipy.sparse as sp
+    if not subsets:
+        raise ValueError("compute_neighbours: no Subsets")
+    parts = []
+    for s in subsets:
+        x = s.samples
+        if not sp.issparse(x):
+            raise ValueError("compute_neighbours: sparse=True needs sparse "
+                             "Subsets")
+        parts.append(x)
+    m = sp.csr_matrix(parts[0] if len(parts) == 1 else
+                      sp.vstack(parts, format="csr"), dtype=np.float64)
+    if not m.has_sorted_indices:
+        m = m.sorted_indices()
+    if m.shape[1] > np.iinfo(np.int32).max:
+        raise ValueError("compute_neighbours: too many features")
+    return m
 
 
 def _concat(subsets, dev):

@@ -253,6 +253,78 @@ __global__ void __launch_bounds__(NB)
     if (live && mine) atomicAdd(cnt + q, mine);
 }
 
+// Sparse epsilon query (the reference's `pairwise_distances` branch of
+// _compute_neighbours, cluster/dbscan/classes.py:130).  sklearn 1.7's
+// _euclidean_distances for fp64 CSR computes
+//   r = ((-2 * q.x) + ||q||^2) + ||x||^2,  max(r, 0),  sqrt
+// with the row norms summed in stored order (_sqeuclidean_row_norms_sparse)
+// and q.x by scipy's csr_matmat: products q_c * x_c accumulated from 0 in
+// the order of q's stored entries.  With sorted indices that is the
+// increasing-column order of the intersection, which a merge of the two
+// sorted rows visits.  One lane per query row; the fit row is wave-uniform
+// (scalar loads), the lane's merge cursor walks its own query row.
+template <int PASS>
+__global__ void __launch_bounds__(NB)
+    k_radius_csr(const int64_t *__restrict__ indptr,
+                 const int32_t *__restrict__ indices,
+                 const double *__restrict__ data, int64_t q0, int64_t nq,
+                 int64_t nx, double eps, int64_t plen,
+                 unsigned long long *__restrict__ cnt,
+                 int64_t *__restrict__ out_i, double *__restrict__ out_d) {
+  const int lane = threadIdx.x & 63;
+  const int64_t qg = (int64_t)blockIdx.x * (NB / 64) +
+                     __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int p = blockIdx.y;
+  const int64_t q = qg * 64 + lane;
+  if (qg * 64 >= nq) return;
+  const bool live = q < nq;
+  const int64_t qa = live ? indptr[q0 + q] : 0;
+  const int64_t qb = live ? indptr[q0 + q + 1] : 0;
+  double xx = 0.0;
+  for (int64_t t = qa; t < qb; ++t) {
+    const double v = data[t];
+    xx += v * v;
+  }
+  const int64_t j0 = (int64_t)p * plen;
+  const int64_t j1 = std::min<int64_t>(nx, j0 + plen);
+  const double e2 = eps * eps;
+  const double e2lo = eps > 0 ? e2 * (1.0 - 0x1.0p-48) : -1.0;
+  const double e2hi = eps > 0 ? e2 * (1.0 + 0x1.0p-48) : -1.0;
+  unsigned long long mine = 0;
+  for (int64_t j = j0; j < j1; ++j) {
+    const int64_t a = indptr[j], b = indptr[j + 1];
+    double yy = 0.0, dot = 0.0;
+    int64_t t = qa;
+    int32_t qc = t < qb ? indices[t] : INT32_MAX;
+    for (int64_t u = a; u < b; ++u) {
+      const int32_t c = indices[u];
+      const double v = data[u];
+      yy += v * v;
+      while (qc < c) {
+        ++t;
+        qc = t < qb ? indices[t] : INT32_MAX;
+      }
+      if (qc == c) dot += data[t] * v;
+    }
+    double r = -2.0 * dot;
+    r += xx;
+    r += yy;
+    r = r < 0.0 ? 0.0 : r;  // np.maximum(r, 0): NaN stays NaN
+    const bool in = r < e2lo || (r <= e2hi && sqrt(r) < eps);
+    if (live && in) {
+      if constexpr (PASS == 0) {
+        ++mine;
+      } else {
+        const unsigned long long at = atomicAdd(cnt + q, 1ull);
+        out_i[at] = j;
+        out_d[at] = sqrt(r);
+      }
+    }
+  }
+  if constexpr (PASS == 0)
+    if (live && mine) atomicAdd(cnt + q, mine);
+}
+
 constexpr int SORT_CAP = 4096;
 
 __device__ __forceinline__ bool key_lt(double da, int64_t ia, double db,
@@ -482,6 +554,17 @@ int radius_args(const double *Q, int64_t nq, int64_t ldq, const double *X,
   return 0;
 }
 
+int radius_csr_args(const int64_t *indptr, const int32_t *indices,
+                    const double *data, int64_t n, int64_t d, int64_t q0,
+                    int64_t nq, double eps) {
+  if (n < 0 || d < 1 || d > INT32_MAX || nq < 0 || q0 < 0 || q0 + nq > n)
+    return fail(DKM_E_ARG, "radius csr: bad n/d/q0/nq");
+  if (std::isnan(eps)) return fail(DKM_E_ARG, "radius csr: eps is NaN");
+  if (n > 0 && (!indptr || (!indices && nq) || (!data && nq)))
+    return fail(DKM_E_ARG, "radius csr: NULL indptr/indices/data");
+  return 0;
+}
+
 }  // namespace
 }  // namespace dkm
 
@@ -614,6 +697,67 @@ int dkm_radius_fill_f64(const double *Q, int64_t nq, int64_t ldq,
   k_seg_sort<<<(unsigned)nq, NB, 0, s>>>(offsets, nq, out_idx, out_dist, sidx,
                                          sdist);
   return check_launch("radius sort");
+}
+
+int dkm_radius_count_csr_f64(const int64_t *indptr, const int32_t *indices,
+                             const double *data, int64_t n, int64_t d,
+                             int64_t q0, int64_t nq, double eps,
+                             int64_t *counts, void *stream) {
+  if (int r = radius_csr_args(indptr, indices, data, n, d, q0, nq, eps))
+    return r;
+  if (nq == 0) return 0;
+  if (!counts) return fail(DKM_E_ARG, "radius csr: NULL counts");
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(counts, 0, (size_t)nq * 8, s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "radius csr: memset");
+  int64_t plen;
+  int P;
+  knn_grid(nq, n, &plen, &P);
+  const dim3 g((unsigned)((nq + 255) / 256), (unsigned)P);
+  k_radius_csr<0><<<g, NB, 0, s>>>(indptr, indices, data, q0, nq, n, eps,
+                                   plen, (unsigned long long *)counts,
+                                   nullptr, nullptr);
+  return check_launch("radius csr count");
+}
+
+int dkm_radius_fill_csr_f64(const int64_t *indptr, const int32_t *indices,
+                            const double *data, int64_t n, int64_t d,
+                            int64_t q0, int64_t nq, double eps,
+                            const int64_t *offsets, void *ws, size_t ws_bytes,
+                            int64_t *out_idx, double *out_dist,
+                            void *stream) {
+  if (int r = radius_csr_args(indptr, indices, data, n, d, q0, nq, eps))
+    return r;
+  if (nq == 0) return 0;
+  if (!offsets || !out_idx || !out_dist)
+    return fail(DKM_E_ARG, "radius csr: NULL offsets/outputs");
+  hipStream_t s = (hipStream_t)stream;
+  int64_t total = 0;
+  if (hipMemcpyAsync(&total, offsets + nq, 8, hipMemcpyDeviceToHost, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "radius csr: reading offsets[nq]");
+  if (total < 0) return fail(DKM_E_ARG, "radius csr: offsets[nq] < 0");
+  if (total == 0) return 0;
+  if (!ws || ws_bytes < dkm_radius_workspace_bytes(nq, total))
+    return fail(DKM_E_WORKSPACE, "radius csr: workspace smaller than "
+                                 "dkm_radius_workspace_bytes()");
+  unsigned long long *cur = (unsigned long long *)ws;
+  int64_t *sidx = (int64_t *)((char *)ws + (size_t)nq * 8);
+  double *sdist = (double *)(sidx + total);
+  if (hipMemcpyAsync(cur, offsets, (size_t)nq * 8, hipMemcpyDeviceToDevice,
+                     s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "radius csr: cursor copy");
+  int64_t plen;
+  int P;
+  knn_grid(nq, n, &plen, &P);
+  const dim3 g((unsigned)((nq + 255) / 256), (unsigned)P);
+  k_radius_csr<1><<<g, NB, 0, s>>>(indptr, indices, data, q0, nq, n, eps,
+                                   plen, cur, out_idx, out_dist);
+  if (int e = check_launch("radius csr fill")) return e;
+  k_seg_sort<<<(unsigned)nq, NB, 0, s>>>(offsets, nq, out_idx, out_dist, sidx,
+                                         sdist);
+  return check_launch("radius csr sort");
 }
 
 }  // extern "C"

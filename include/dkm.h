@@ -352,6 +352,23 @@ int dkm_radius_fill_f64(const double *Q, int64_t nq, int64_t ldq,
                         double eps, const int64_t *offsets, void *ws,
                         size_t ws_bytes, int64_t *out_idx, double *out_dist,
                         void *stream);
+/* Sparse epsilon query, replacing the `pairwise_distances` branch of
+ * _compute_neighbours (dislib/cluster/dbscan/classes.py:130, sparse=True):
+ * query rows q0 .. q0+nq of the CSR matrix (indptr[n+1] int64, indices
+ * int32 sorted within each row, data fp64, n rows, d columns) against all
+ * n rows.  Distance = sklearn 1.7 euclidean_distances for fp64 CSR:
+ * sqrt(max(((-2 q.x) + ||q||^2) + ||x||^2, 0)), row norms summed in stored
+ * order, q.x by scipy csr_matmat order (increasing column of the
+ * intersection).  Same two steps, offsets and workspace as the dense pair. */
+int dkm_radius_count_csr_f64(const int64_t *indptr, const int32_t *indices,
+                             const double *data, int64_t n, int64_t d,
+                             int64_t q0, int64_t nq, double eps,
+                             int64_t *counts, void *stream);
+int dkm_radius_fill_csr_f64(const int64_t *indptr, const int32_t *indices,
+                            const double *data, int64_t n, int64_t d,
+                            int64_t q0, int64_t nq, double eps,
+                            const int64_t *offsets, void *ws, size_t ws_bytes,
+                            int64_t *out_idx, double *out_dist, void *stream);
 
 /* ------------------------------------------------------------------------
  * Dataset loaders.  HOST functions: `buf`

@@ -128,3 +128,74 @@ def compute_neighbours(epsilon, min_samples, begin_idx, end_idx, samples):
         neighbour_list.append(neigh)
         core_points.append(neigh.size >= min_samples)
     return neighbour_list, core_points
+
+
+# --------------------------------------------------------------------------
+# sparse epsilon query (cluster/dbscan/classes.py:124-141, sparse=True)
+# --------------------------------------------------------------------------
+def _seq_row_sums(indptr, vals):
+    """Per-row sums of ``vals`` (one per stored entry) accumulated from 0 in
+    stored order -- the loop of sklearn's ``_sqeuclidean_row_norms_sparse``;
+    vectorised over rows, one entry position at a time."""
+    n = indptr.size - 1
+    lens = np.diff(indptr)
+    acc = np.zeros(n)
+    for k in range(int(lens.max()) if n else 0):
+        rows = np.nonzero(lens > k)[0]
+        acc[rows] = acc[rows] + vals[indptr[rows] + k]
+    return acc
+
+
+def csr_sq_distances(indptr, indices, data, q):
+    """``pairwise_distances(row q, X) ** 2`` before the sqrt, as sklearn 1.7
+    (``metrics/pairwise.py`` ``_euclidean_distances``, fp64) computes it for
+    CSR input with sorted indices: ``XX = row_norms(q)``, ``YY =
+    row_norms(X)`` (stored-order sums), ``D = -2 * (q @ X.T)`` (scipy
+    ``csr_matmat``: the products ``q_c * x_c`` of the matching columns summed
+    from 0 in q's stored order), ``D += XX``, ``D += YY``,
+    ``np.maximum(D, 0)``."""
+    indptr = np.asarray(indptr, np.int64)
+    indices = np.asarray(indices)
+    data = np.asarray(data, np.float64)
+    yy = _seq_row_sums(indptr, data * data)
+    qa, qb = indptr[q], indptr[q + 1]
+    qi, qv = indices[qa:qb], data[qa:qb]
+    xx = 0.0
+    for v in qv:
+        xx += v * v
+    # the matching query entry of every stored entry (or none)
+    if qi.size:
+        pos = np.minimum(np.searchsorted(qi, indices), qi.size - 1)
+        match = qi[pos] == indices
+        with np.errstate(all="ignore"):
+            prod = qv[pos] * data
+    else:
+        match = np.zeros(indices.size, bool)
+        prod = np.zeros(indices.size)
+    n = indptr.size - 1
+    lens = np.diff(indptr)
+    dot = np.zeros(n)
+    for k in range(int(lens.max()) if n else 0):
+        rows = np.nonzero(lens > k)[0]
+        at = indptr[rows] + k
+        m = match[at]
+        dot[rows[m]] = dot[rows[m]] + prod[at[m]]
+    r = -2.0 * dot
+    r += xx
+    r += yy
+    return np.maximum(r, 0.0)
+
+
+def compute_neighbours_csr(epsilon, min_samples, begin_idx, end_idx,
+                           indptr, indices, data):
+    """Sparse ``_compute_neighbours``: same lists and flags as the dense
+    form, distances by :func:`csr_sq_distances` then ``sqrt``."""
+    n = len(indptr) - 1
+    neighbour_list, core_points = [], []
+    for q in range(*slice(begin_idx, end_idx).indices(n)):
+        dist = np.sqrt(csr_sq_distances(indptr, indices, data, q))
+        neigh = np.where(dist < epsilon)[0]
+        neigh = neigh[np.lexsort((neigh, dist[neigh]))]
+        neighbour_list.append(neigh)
+        core_points.append(neigh.size >= min_samples)
+    return neighbour_list, core_points

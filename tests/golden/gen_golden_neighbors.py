@@ -14,7 +14,8 @@ Run in the development container only:
 imports the reference under the sequential PyCOMPSs stub.  Nothing of the
 reference is copied: inputs are seeded synthetic matrices (stored, they are
 small), outputs are what the reference returned.  Writes
-``neighbors_ref.npz``.
+``neighbors_ref.npz`` and ``neighbors_sparse_ref.npz`` (the epsilon query
+on sparse Subsets).
 """
 import os
 import subprocess
@@ -41,6 +42,14 @@ DB_CASES = [
     ("db_d10", 300, 10, 75, 1.6, 8, 50, 250),
     ("db_d130", 150, 130, 50, 16.3, 3, 10, 140),
     ("db_none", 120, 3, 40, 1e-3, 2, 0, 120),        # only the point itself
+]
+# sparse Subsets (the pairwise_distances branch, classes.py:130):
+# (name, n, d, subset, density, epsilon, min_samples, begin, end)
+DB_SPARSE_CASES = [
+    ("dbs_small", 200, 50, 50, 0.1, 0.8, 3, 0, 200),
+    ("dbs_wide", 300, 2000, 100, 0.005, 2.3, 2, 20, 280),   # ~10 nnz / row
+    ("dbs_empty", 150, 30, 50, 0.03, 0.3, 2, 0, 150),       # empty rows
+    ("dbs_blobs", 240, 20, 60, None, 5.5, 4, 30, 210),      # thresholded blobs
 ]
 
 
@@ -87,6 +96,35 @@ def generate():
         print("dbscan", name, int(lens.sum()), "neighbours")
     np.savez_compressed(os.path.join(HERE, "neighbors_ref.npz"), **out)
     print("wrote neighbors_ref.npz")
+    import scipy.sparse as sp
+    out = {}
+    for i, (name, n, d, sub, dens, eps, ms, b, e) in enumerate(
+            DB_SPARSE_CASES):
+        rng = np.random.default_rng(300 + i)
+        if dens is None:
+            x = _data(rng, n, d, "blobs")
+            x[np.abs(x) < 1.0] = 0.0
+            x = sp.csr_matrix(x)
+        else:
+            x = sp.random(n, d, density=dens, format="csr", random_state=rng,
+                          data_rvs=lambda k: rng.uniform(-1, 1, k))
+        x.sort_indices()
+        ds = load_data(x, subset_size=sub)
+        nl, cp = _compute_neighbours(eps, ms, True, b, e, *list(ds))
+        lens = np.array([len(v) for v in nl], dtype=np.int64)
+        out[name + "__indptr"] = x.indptr.astype(np.int64)
+        out[name + "__indices"] = x.indices.astype(np.int32)
+        out[name + "__data"] = x.data
+        out[name + "__shape"] = np.array(x.shape, dtype=np.int64)
+        out[name + "__meta"] = np.array([sub, eps, ms, b, e], dtype=np.float64)
+        out[name + "__offsets"] = np.concatenate([[0], np.cumsum(lens)])
+        out[name + "__neigh"] = (np.concatenate(nl).astype(np.int64)
+                                 if len(nl) else np.zeros(0, np.int64))
+        out[name + "__core"] = np.asarray(cp, dtype=bool)
+        print("dbscan sparse", name, x.nnz, "nnz", int(lens.sum()),
+              "neighbours")
+    np.savez_compressed(os.path.join(HERE, "neighbors_sparse_ref.npz"), **out)
+    print("wrote neighbors_sparse_ref.npz")
 
 
 def main():

@@ -170,3 +170,63 @@ def test_epsilon_query_vs_oracle(n, d, eps, b, e, grid):
     for r in range(len(nl)):
         assert np.array_equal(nl[r], onl[r]), r
     assert cp == ocp
+
+
+# --- sparse epsilon query (classes.py:130, sparse=True) --------------------
+from tests.test_neighbors_golden import (DBS, assert_same_up_to_ties,  # noqa
+                                         sparse_case)
+
+
+def _eps_query_csr(m, sub, eps, ms, b, e):
+    from dislib_amd.cluster.dbscan import compute_neighbours
+    from dislib_amd.data import load_data
+    return compute_neighbours(eps, ms, True, b, e,
+                              *list(load_data(m, subset_size=sub)))
+
+
+@pytest.mark.parametrize("name", DBS)
+def test_sparse_epsilon_query_reference_golden(name):
+    import scipy.sparse as sp
+    ip, ix, dv, shape, meta, off, ref, core = sparse_case(name)
+    sub, eps, ms, b, e = meta
+    m = sp.csr_matrix((dv, ix, ip), shape=tuple(shape))
+    nl, cp = _eps_query_csr(m, int(sub), eps, ms, int(b), int(e))
+    assert len(nl) == len(off) - 1
+    for r, v in enumerate(nl):
+        assert_same_up_to_ties(v, ref[off[r]:off[r + 1]], ip, ix, dv,
+                               int(b) + r, (name, r))
+    assert cp == list(core)
+
+
+@pytest.mark.parametrize("n,d,dens,eps,b,e,kind", [
+    (3000, 500, 0.02, 2.0, 100, 2900, "uniform"),   # ~10 nnz per row
+    (2000, 40, 0.3, 1.5, 0, 2000, "grid"),          # ties on integer values
+    (1200, 100000, 0.0001, 1.2, 0, 1200, "uniform"),  # mostly empty rows
+    (5000, 8, 0.5, 1e9, 0, 3, "uniform"),           # lists of 5000 (> LDS)
+    (600, 30, 0.2, 0.0, 0, 600, "grid"),            # eps = 0: none
+    (600, 30, 0.2, 2.0, 0, 600, "unsorted"),        # unsorted column order
+    (400, 20, 0.3, 3.0, 0, 400, "big"),             # 1e200: overflow -> inf
+])
+def test_sparse_epsilon_query_vs_oracle(n, d, dens, eps, b, e, kind):
+    import scipy.sparse as sp
+    rng = np.random.default_rng(n + d)
+    rvs = {"grid": lambda k: rng.integers(1, 4, k).astype(np.float64),
+           "big": lambda k: rng.choice([1.0, -2.0, 1e200], k)}.get(
+        kind, lambda k: rng.uniform(-1, 1, k))
+    m = sp.random(n, d, density=dens, format="csr", random_state=rng,
+                  data_rvs=rvs)
+    m.sort_indices()
+    ip, ix, dv = m.indptr.astype(np.int64), m.indices, m.data
+    if kind == "unsorted":  # same matrix, entries reversed within rows
+        perm = np.concatenate([np.arange(ip[i + 1] - 1, ip[i] - 1, -1)
+                               for i in range(n)]).astype(np.int64)
+        m = sp.csr_matrix((dv[perm], ix[perm], ip), shape=m.shape)
+        assert not m.has_sorted_indices
+    nl, cp = _eps_query_csr(m, 250, eps, 4, b, e)
+    onl, ocp = orc.compute_neighbours_csr(eps, 4, b, e, ip, ix, dv)
+    assert len(nl) == len(onl)
+    for r in range(len(nl)):
+        assert np.array_equal(nl[r], onl[r]), r
+    assert cp == ocp
+    if kind == "grid" and eps > 0:
+        assert sum(len(v) for v in nl) > n  # more than the points themselves

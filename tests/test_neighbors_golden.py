@@ -65,3 +65,53 @@ def test_oracle_epsilon_query_is_the_reference(name):
     for r, v in enumerate(nl):
         assert np.array_equal(v, ref[off[r]:off[r + 1]]), (name, r)
     assert np.array_equal(np.array(cp), G[name + "__core"])
+
+
+GS = np.load(os.path.join(os.path.dirname(__file__), "golden",
+                          "neighbors_sparse_ref.npz"))
+DBS = sorted({k.split("__")[0] for k in GS.files})
+
+
+def sparse_case(name):
+    """(indptr, indices, data, shape, meta, offsets, neigh, core) of a
+    sparse epsilon-query golden (classes.py:130, sparse=True)."""
+    return tuple(GS[name + "__" + f] for f in (
+        "indptr", "indices", "data", "shape", "meta", "offsets", "neigh",
+        "core"))
+
+
+@pytest.mark.parametrize("name", DBS)
+def test_oracle_sparse_epsilon_query_is_the_reference(name):
+    ip, ix, dv, shape, meta, off, ref, core = sparse_case(name)
+    sub, eps, ms, b, e = meta
+    nl, cp = orc.compute_neighbours_csr(eps, ms, int(b), int(e), ip, ix, dv)
+    assert len(nl) == len(off) - 1
+    for r, v in enumerate(nl):
+        assert_same_up_to_ties(v, ref[off[r]:off[r + 1]], ip, ix, dv,
+                               int(b) + r, (name, r))
+    assert np.array_equal(np.array(cp), core)
+
+
+def assert_same_up_to_ties(v, w, ip, ix, dv, q, what):
+    """Identical lists, except that runs of exactly equal distances may be
+    permuted: the reference's np.argsort (introsort) does not order equal
+    keys by index (dbs_empty: empty rows, all at distance 0)."""
+    if np.array_equal(v, w):
+        return
+    dist = np.sqrt(orc.csr_sq_distances(ip, ix, dv, q))
+    assert np.array_equal(np.sort(v), np.sort(w)), what
+    assert np.array_equal(dist[v], dist[w]), what
+
+
+def test_oracle_sparse_distances_are_sklearns_expansion():
+    """The restated distances against sklearn's own pairwise_distances on
+    the golden inputs (bit for bit, the sqrt of the restated squares)."""
+    sk = pytest.importorskip("sklearn.metrics")
+    sp = pytest.importorskip("scipy.sparse")
+    for name in DBS:
+        ip, ix, dv, shape, *_ = sparse_case(name)
+        m = sp.csr_matrix((dv, ix, ip), shape=tuple(shape))
+        for q in (0, 7, int(shape[0]) - 1):
+            want = sk.pairwise_distances(m[q], m).ravel()
+            got = np.sqrt(orc.csr_sq_distances(ip, ix, dv, q))
+            assert np.array_equal(got, want), (name, q)
