@@ -38,11 +38,20 @@ def main():
     p.add_argument("--eps-n", type=int, default=400_000)
     p.add_argument("--eps-q", type=int, default=100_000)
     p.add_argument("--eps", type=float, default=0.25)
+    p.add_argument("--sp-n", type=int, default=200_000)
+    p.add_argument("--sp-d", type=int, default=10_000)
+    p.add_argument("--sp-nnz", type=int, default=10)
+    p.add_argument("--sp-q", type=int, default=50_000)
+    p.add_argument("--sp-eps", type=float, default=2.3)
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--no-cpu", action="store_true")
     a = p.parse_args()
 
     rng = np.random.default_rng(0)
+    import scipy.sparse as sp
+    xs = sp.random(a.sp_n, a.sp_d, density=a.sp_nnz / a.sp_d, format="csr",
+                   random_state=rng)
+    xs.sort_indices()
     xf = rng.random((a.nfit, a.d))
     xq = rng.random((a.nq, a.d))
     xe = rng.random((a.eps_n, a.d))
@@ -69,6 +78,18 @@ def main():
                       "sample": "%d query rows against %d rows, the "
                                 "reference's per-sample numpy loop"
                                 % (m, a.eps_n)}
+        from sklearn.metrics import pairwise_distances
+        m = 100
+        t0 = time.perf_counter()
+        for i in range(m):
+            dist = pairwise_distances(xs[i], xs).ravel()
+            np.argsort(dist[np.where(dist < a.sp_eps)[0]])
+        el = time.perf_counter() - t0
+        cpu["eps_csr"] = {"value": m / el, "unit": "queries/s", "cores": 1,
+                          "kind": "reference", "seconds": el,
+                          "sample": "%d query rows against %d CSR rows, the "
+                                    "reference's per-sample sklearn "
+                                    "pairwise_distances loop" % (m, a.sp_n)}
 
     import torch
     from dislib_amd.cluster.dbscan import compute_neighbours
@@ -127,7 +148,30 @@ def main():
     if "eps" in cpu:
         eps["cpu_baseline"] = cpu["eps"]
         eps["gpu_over_cpu"] = eps["value"] / cpu["eps"]["value"]
-    print(json.dumps({"kneighbors": knn, "epsilon_query": eps}), flush=True)
+    sp_subs = list(load_data(xs, subset_size=a.subset))
+    compute_neighbours(a.sp_eps, 5, True, 0, a.sp_q, *sp_subs)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        nl, _ = compute_neighbours(a.sp_eps, 5, True, 0, a.sp_q, *sp_subs)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    t = min(ts)
+    pairs = float(a.sp_q) * a.sp_n
+    eps_csr = {"workload": "DBSCAN epsilon query, sparse: %d queries x %d "
+                           "CSR rows, d=%d, %d nnz/row, eps=%g"
+                           % (a.sp_q, a.sp_n, a.sp_d, a.sp_nnz, a.sp_eps),
+               "value": a.sp_q / t, "unit": "queries/s", "seconds": t,
+               "pairs_per_s": pairs / t,
+               "neighbours": int(sum(len(v) for v in nl)),
+               "includes": "host concatenation + upload of the CSR arrays, "
+                           "two passes, the sort and the copy back"}
+    if "eps_csr" in cpu:
+        eps_csr["cpu_baseline"] = cpu["eps_csr"]
+        eps_csr["gpu_over_cpu"] = eps_csr["value"] / cpu["eps_csr"]["value"]
+    print(json.dumps({"kneighbors": knn, "epsilon_query": eps,
+                      "epsilon_query_csr": eps_csr}), flush=True)
 
 
 if __name__ == "__main__":
