@@ -200,7 +200,7 @@ def test_sparse_epsilon_query_reference_golden(name):
 
 @pytest.mark.parametrize("n,d,dens,eps,b,e,kind", [
     (3000, 500, 0.02, 2.0, 100, 2900, "uniform"),   # ~10 nnz per row
-    (2000, 40, 0.3, 1.5, 0, 2000, "grid"),          # ties on integer values
+    (2000, 8, 0.3, 2.0, 0, 2000, "grid"),           # ties on integer values
     (1200, 100000, 0.0001, 1.2, 0, 1200, "uniform"),  # mostly empty rows
     (5000, 8, 0.5, 1e9, 0, 3, "uniform"),           # lists of 5000 (> LDS)
     (600, 30, 0.2, 0.0, 0, 600, "grid"),            # eps = 0: none
