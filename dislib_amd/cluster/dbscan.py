@@ -72,9 +72,9 @@ def compute_neighbours(epsilon, min_samples, sparse, begin_idx, end_idx,
 
 def _compute_neighbours_csr(epsilon, min_samples, begin_idx, end_idx,
                             subsets, device):
+    m = _concat_csr(subsets)
     t = torch()
     dev = resolve(device)
-    m = _concat_csr(subsets)
     n, d = m.shape
     b, e = _slice_bounds(begin_idx, end_idx, n)
     nq = e - b

@@ -180,3 +180,25 @@ def test_device_must_be_a_gpu():
     from dislib_amd import _device
     with pytest.raises(ValueError, match="ROCm GPU"):
         _device.resolve("cpu")
+
+
+def test_sparse_epsilon_query_host_checks():
+    """The sparse epsilon query (dbscan classes.py:130) rejects dense
+    Subsets before any device call, and concatenates CSR Subsets into one
+    matrix with sorted column indices (the order scipy's products follow)."""
+    import scipy.sparse as sp
+    from dislib_amd.cluster.dbscan import _concat_csr, compute_neighbours
+    from dislib_amd.data import load_data
+    with pytest.raises(ValueError):
+        compute_neighbours(1.0, 2, True, 0, 5,
+                           *list(load_data(np.zeros((10, 3)), subset_size=5)))
+    rng = np.random.default_rng(3)
+    m = sp.random(50, 20, density=0.3, format="csr", random_state=rng)
+    ip, ix, dv = m.indptr, m.indices.copy(), m.data.copy()
+    for i in range(50):          # reverse the entries of every row
+        ix[ip[i]:ip[i + 1]] = ix[ip[i]:ip[i + 1]][::-1].copy()
+        dv[ip[i]:ip[i + 1]] = dv[ip[i]:ip[i + 1]][::-1].copy()
+    u = sp.csr_matrix((dv, ix, ip), shape=m.shape)
+    c = _concat_csr(list(load_data(u, subset_size=15)))
+    assert c.has_sorted_indices
+    assert (c != m).nnz == 0
