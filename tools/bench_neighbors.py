@@ -42,7 +42,7 @@ def main():
     p.add_argument("--sp-d", type=int, default=10_000)
     p.add_argument("--sp-nnz", type=int, default=10)
     p.add_argument("--sp-q", type=int, default=50_000)
-    p.add_argument("--sp-eps", type=float, default=2.3)
+    p.add_argument("--sp-eps", type=float, default=1.5)
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--no-cpu", action="store_true")
     a = p.parse_args()
