@@ -119,6 +119,7 @@ class DeviceData:
             m = sp.vstack(mats, format="csr") if mats else \
                 sp.csr_matrix((0, self.d))
         # keep each row's stored order: it is the reference's dot order
+        assert_all_finite(m.data)
         self.dtype = np.float64
         self.indptr = t.from_numpy(m.indptr.astype(np.int64)).to(self.device)
         self.indices = t.from_numpy(m.indices.astype(np.int32)).to(
@@ -161,6 +162,19 @@ class DeviceData:
     def subset_slices(self):
         return [(int(a), int(b)) for a, b in zip(self.offsets[:-1],
                                                  self.offsets[1:])]
+
+
+def assert_all_finite(values):
+    """The sparse path's input check: the reference computes its sparse
+    distances with sklearn's ``pairwise_distances`` (kmeans/base.py:169,
+    196; dbscan/classes.py:130), whose ``check_array`` raises ValueError on
+    NaN or inf in either operand -- with these messages."""
+    v = np.asarray(values)
+    if v.size and not np.isfinite(v).all():
+        if np.isnan(v).any():
+            raise ValueError("Input contains NaN.")
+        raise ValueError("Input contains infinity or a value too large for "
+                         "dtype('float64').")
 
 
 def _adjacent_view(xs):

@@ -28,6 +28,7 @@ import numpy as np
 
 from .. import _lib
 from .._device import _is_torch, on, ptr, resolve, stream_ptr, torch
+from .._device import assert_all_finite as _device_assert_finite
 
 
 def compute_neighbours(epsilon, min_samples, sparse, begin_idx, end_idx,
@@ -131,6 +132,21 @@ def _concat_csr(subsets):
         m = m.sorted_indices()
     if m.shape[1] > np.iinfo(np.int32).max:
         raise ValueError("compute_neighbours: too many features")
+    # duplicate column entries in a row (legal while a scipy matrix is not
+    # in canonical format): scipy's csr_matmat multiplies every stored pair
+    # in stored order, which the kernel's merge of two sorted rows does not
+    # reproduce -- refuse them loudly instead of returning other distances
+    ind = m.indices
+    if ind.size > 1:
+        same = ind[1:] == ind[:-1]
+        if same.any():
+            row_start = np.zeros(ind.size, bool)
+            row_start[m.indptr[:-1][np.diff(m.indptr) > 0]] = True
+            if (same & ~row_start[1:]).any():
+                raise ValueError(
+                    "compute_neighbours: sparse samples hold duplicate "
+                    "column entries; call sum_duplicates() on them first")
+    _device_assert_finite(m.data)
     return m
 
 

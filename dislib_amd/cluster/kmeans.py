@@ -102,6 +102,9 @@ class KMeans:
         k, d = centers.shape
         if d != dd.d:
             raise ValueError("centers have %d features, data %d" % (d, dd.d))
+        if dd.sparse:
+            from .._device import assert_all_finite
+            assert_all_finite(centers)
         C = t.from_numpy(np.ascontiguousarray(centers)).to(dd.device)
         ws = Workspace(k, d, min(dd.n, 1 << 24), dd.device)
         labels = t.empty(dd.n, dtype=t.int32, device=dd.device)

@@ -228,18 +228,21 @@ __global__ void __launch_bounds__(BLOCK)
     for (int t = 0; t < MAXD; ++t) x[t] = t < d ? ld_x(xr + t) : 0.0;
     // argmin over sqrt'd distances, first index on ties (np.argmin); sqrt
     // is monotone, so a centre can only win (or tie) when s < best_s.
-    double best_s = exact_sqdist_reg<MAXD>(x, cl, d);
-    double best = sqrt(best_s);
+    // NaN distances rank first (np.argmin's first-NaN rule): argmin_key
+    const double s0 = exact_sqdist_reg<MAXD>(x, cl, d);
+    double best_s = argmin_key(s0);
+    double best = argmin_key(sqrt(s0));
     int bi = 0;
     for (int j = 1; j < k; ++j) {
       const double s = exact_sqdist_reg<MAXD>(x, cl + (int64_t)j * d, d);
-      if (s < best_s) {
-        const double dist = sqrt(s);
+      const double ks = argmin_key(s);
+      if (ks < best_s) {
+        const double dist = argmin_key(sqrt(s));
         if (dist < best) {
           best = dist;
           bi = j;
         }
-        best_s = s;
+        best_s = ks;
       }
     }
     const int prev = (amode & AM_DELTA) ? labels[i] : -1;
@@ -258,18 +261,20 @@ __global__ void __launch_bounds__(BLOCK)
 template <class TX>
 __device__ __forceinline__ int exact_label_lane(const TX *xr, int d,
                                                 const double *C, int k) {
-  double best_s = pw_sum(SqDiff<TX>{xr, C}, d);
-  double best = sqrt(best_s);
+  const double s0 = pw_sum(SqDiff<TX>{xr, C}, d);
+  double best_s = argmin_key(s0);
+  double best = argmin_key(sqrt(s0));
   int bi = 0;
   for (int j = 1; j < k; ++j) {
     const double s = pw_sum(SqDiff<TX>{xr, C + (int64_t)j * d}, d);
-    if (s < best_s) {
-      const double dist = sqrt(s);
+    const double ks = argmin_key(s);
+    if (ks < best_s) {
+      const double dist = argmin_key(sqrt(s));
       if (dist < best) {
         best = dist;
         bi = j;
       }
-      best_s = s;
+      best_s = ks;
     }
   }
   return bi;
@@ -512,7 +517,7 @@ __device__ __forceinline__ bool resolve_lane(
     for (int jc = 0; jc < k; ++jc) {
       if (sane && !(score(jc) <= lim)) continue;
       const SqDiffT<TX> f{xr, ct64 + jc, ct_ld(k)};
-      const double dist = sqrt(pw_leaf(f, 0, d));
+      const double dist = argmin_key(sqrt(pw_leaf(f, 0, d)));
       if (dist < best || bi < 0) {
         best = dist;
         bi = jc;
@@ -1941,7 +1946,7 @@ __global__ void __launch_bounds__(BLOCK)
       r = r + __shfl_xor(r, 1, 64);
       r = r + __shfl_xor(r, 2, 64);
       r = r + __shfl_xor(r, 4, 64);
-      const double dist = sqrt(r);
+      const double dist = argmin_key(sqrt(r));
       const double o = __shfl_xor(dist, 8, 64);  // the other candidate
       if (live && cs == 0 && j == 0)
         lab_out[si] = (o < dist || (o == dist && c2 < c1)) ? c2 : c1;
@@ -1993,7 +1998,7 @@ __global__ void __launch_bounds__(BLOCK)
         r = r + __shfl_xor(r, 1, 64);
         r = r + __shfl_xor(r, 2, 64);
         r = r + __shfl_xor(r, 4, 64);
-        const double dc = sqrt(r);
+        const double dc = argmin_key(sqrt(r));
         if (dc < best || (dc == best && c < bi) || bi < 0) {
           best = dc;
           bi = c;
@@ -2254,7 +2259,8 @@ __global__ void __launch_bounds__(BLOCK)
       int bi = 0x7fffffff;  // lanes without a centre never win
       for (int jc = lane; jc < k; jc += 64) {
         const SqDiffT<TX> f{xr, v.ct64 + jc, ct_ld(k)};
-        const double dist = sqrt(SMALL ? pw_leaf(f, 0, d) : pw_sum(f, d));
+        const double dist =
+            argmin_key(sqrt(SMALL ? pw_leaf(f, 0, d) : pw_sum(f, d)));
         if (dist < best || bi == 0x7fffffff) {
           best = dist;
           bi = jc;

@@ -646,7 +646,8 @@ __global__ void __launch_bounds__(256)
         const int2 c = pp[q];
         if (!(__int_as_float(c.x) <= lim)) continue;
         const double dist =
-            sqrt(wave_sqdist(xr, C + (int64_t)c.y * d, d, tab, tot, lane));
+            argmin_key(sqrt(wave_sqdist(xr, C + (int64_t)c.y * d, d, tab, tot,
+                                        lane)));
         if (lab == 0x7fffffff || dist < best || (dist == best && c.y < lab)) {
           best = dist;
           lab = c.y;
@@ -658,7 +659,7 @@ __global__ void __launch_bounds__(256)
         const int2 c = pp[q];
         if (!(__int_as_float(c.x) <= lim)) continue;
         const double dist =
-            sqrt(pw_sum(SqDiff<TX>{xr, C + (int64_t)c.y * d}, d));
+            argmin_key(sqrt(pw_sum(SqDiff<TX>{xr, C + (int64_t)c.y * d}, d)));
         if (lab == 0x7fffffff || dist < best || (dist == best && c.y < lab)) {
           best = dist;
           lab = c.y;

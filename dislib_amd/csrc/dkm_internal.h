@@ -393,6 +393,14 @@ __device__ __forceinline__ double exact_sqdist_reg(const double (&x)[MAXD],
   return res;
 }
 
+// np.argmin's order on distances (base.py:173,200): a NaN ranks before every
+// number (the FIRST NaN wins), otherwise first index of the minimum.  The
+// distances are sqrt'd sums of squares, so every non-NaN one is >= 0 and
+// mapping NaN to -1 gives that order under plain (value, index) compares.
+__device__ __forceinline__ double argmin_key(double v) {
+  return v != v ? -1.0 : v;
+}
+
 // (dist, idx) lexicographic minimum across a wave: first index wins ties.
 __device__ __forceinline__ void wave_argmin(double &dist, int &idx) {
 #pragma unroll

@@ -316,7 +316,9 @@ __global__ void __launch_bounds__(256)
       double dd = -2.0 * dot;
       dd = dd + xx;
       dd = dd + yy[j];
-      const double dist = sqrt(dd > 0.0 ? dd : 0.0);
+      // np.maximum(dd, 0) keeps a NaN (sklearn's clamp), then the argmin
+      // key ranks it first (np.argmin)
+      const double dist = argmin_key(sqrt(dd > 0.0 || dd != dd ? dd : 0.0));
       if (dist < best || bi == 0x7fffffff) {
         best = dist;
         bi = j;

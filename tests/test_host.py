@@ -202,3 +202,35 @@ def test_sparse_epsilon_query_host_checks():
     c = _concat_csr(list(load_data(u, subset_size=15)))
     assert c.has_sorted_indices
     assert (c != m).nnz == 0
+
+
+def test_sparse_epsilon_query_refuses_duplicates_and_nonfinite():
+    """a non-canonical CSR row with a duplicate column would get
+    other products than scipy's csr_matmat (every stored pair): refused
+    loudly; equal columns in DIFFERENT rows are fine.  NaN / inf raise like
+    sklearn's pairwise_distances input check (dbscan classes.py:130)."""
+    from dislib_amd.cluster.dbscan import _concat_csr
+    from dislib_amd.data import load_data
+    dup = sp.csr_matrix((np.array([1., 2, 3, 4]), np.array([1, 1, 0, 2]),
+                         np.array([0, 2, 2, 4])), shape=(3, 3))
+    with pytest.raises(ValueError, match="duplicate"):
+        _concat_csr(list(load_data(dup, subset_size=3)))
+    ok = sp.csr_matrix((np.array([1., 2, 3, 4]), np.array([1, 2, 2, 3]),
+                        np.array([0, 2, 2, 4])), shape=(3, 4))
+    assert _concat_csr(list(load_data(ok, subset_size=3))).nnz == 4
+    for bad, msg in ((np.nan, "NaN"), (np.inf, "infinity")):
+        b = ok.copy()
+        b.data[1] = bad
+        with pytest.raises(ValueError, match=msg):
+            _concat_csr(list(load_data(b, subset_size=3)))
+
+
+def test_sparse_kmeans_nonfinite_raises_before_the_device():
+    """The sparse k-means path raises sklearn's ValueError on NaN / inf
+    samples (base.py:169 -> pairwise_distances' check_array)."""
+    from dislib_amd._device import assert_all_finite
+    assert_all_finite(np.array([0.0, 1.0]))
+    with pytest.raises(ValueError, match="Input contains NaN"):
+        assert_all_finite(np.array([0.0, np.nan, np.inf]))
+    with pytest.raises(ValueError, match="infinity"):
+        assert_all_finite(np.array([-np.inf]))
