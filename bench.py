@@ -273,13 +273,15 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
            "collective": ("libdkm-rccl" if info else "torch.distributed")
            if world > 1 else "none",
            "rccl_ranks": info[0] if info else None,
-           "pruned": st.pstate is not None,
-           # the sample image the screen streamed (dkm_x_image_*), if any
-           "image_kind": max(st.dd.images) if getattr(st.dd, "images", None)
-           else 0,
-           # samples screened per pruned iteration (whole fit; the first is
-           # the bounds' initial full pass)
-           "active": list(st.active)}
+           # the sample image the screen streamed: the fit's label-sorted
+           # image (3), else the dataset's cached one (dkm_x_image_*), if any
+           "image_kind": 3 if getattr(st, "simg", None) is not None else
+           (max(st.dd.images) if getattr(st.dd, "images", None) else 0),
+           # single-product screen counters (threshold tiles, decided,
+           # centre blocks screened over the sorted image), whole fit
+           "counters": st.screened_blocks() if not csr_nnz and
+           getattr(st, "sorting", False) else None,
+           "nkb": (k + 31) // 32}
     del st, ds, X
     torch.cuda.empty_cache()
     return out
@@ -302,12 +304,16 @@ def traffic_for(n, d, k, path=None):
     return None
 
 
-def prune_fields(r, n):
-    """Bound-based skipping (dkm_assign_pruned): samples screened per pruned
-    iteration of the whole fit, as fractions of the shard."""
-    if not r.get("pruned"):
+def skip_fields(r):
+    """Block skipping over the label-sorted image: the
+    fraction of (tile, 32-centre block) pairs the threshold passes of the
+    whole fit screened."""
+    c = r.get("counters")
+    if not c or not c[0]:
         return None
-    return {"screened_frac": [round(a / n, 5) for a in r["active"]]}
+    return {"threshold_tiles": c[0], "tiles_decided": c[1],
+            "blocks_screened": c[2],
+            "screened_frac": c[2] / (c[0] * r["nkb"])}
 
 
 def fit_fields(r, n, world):
@@ -362,6 +368,8 @@ def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
             sb = 4096 // 32 + 4 + 8
         elif ik == 1:
             sb = (d + 15) // 16 * 1024 // 32 + 4 + 8
+        elif ik == 3:          # + the row's sample index and label copy
+            sb = (d + 15) // 16 * 1024 // 32 + 4 + 8 + 4
         else:
             sb = es * d + 8
         out = {"bound": "hbm", "achieved": b / sec / 1e9,
@@ -381,7 +389,9 @@ def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
                "image": {0: "none (X converted in the screen)",
                          1: "bf16 single (resident, built in the fit)",
                          2: "bf16 hi+lo split (resident, built in the "
-                            "fit)"}[ik],
+                            "fit)",
+                         3: "bf16 single, rows grouped by label (built in "
+                            "the fit; block skipping)"}[ik],
                "streamed_bytes_per_sample": sb,
                "streamed_gbs": n * sb / sec / 1e9,
                "streamed_frac": n * sb / sec / 1e9 / HBM_PEAK_GBS}
@@ -503,7 +513,7 @@ def main():
                               traffic=None if f32 or nnz else
                               traffic_for(n, d, k)),
              "rechecked_samples": rr["rechecked"],
-             "pruning": prune_fields(rr, n)}
+             "block_skip": skip_fields(rr)}
         e.update(fit_fields(rr, n, world))
         if nnz:
             e["nnz_per_row"] = nnz
@@ -554,7 +564,7 @@ def main():
                    "parallelism": "dp%d" % world},
         "roofline": rf,
         "rechecked_samples": r["rechecked"],
-        "pruning": prune_fields(r, a.n),
+        "block_skip": skip_fields(r),
         "collective": r["collective"],
     }
     out.update(fit_fields(r, a.n, world))

@@ -158,6 +158,12 @@ class DeviceData:
         self.images[kind] = img
         return img, kind
 
+    def drop_images(self):
+        """Free the resident sample images (up to 16.5 GB at C3): later
+        calls convert X in the screen, or build an image again."""
+        self.images = {}
+        self._image_failed = set()
+
     # -- helpers -----------------------------------------------------------
     def subset_slices(self):
         return [(int(a), int(b)) for a, b in zip(self.offsets[:-1],
@@ -235,7 +241,19 @@ def prepare(C, ws, acc, csr=False):
                "dkm_prepare_centers")
 
 
-def partial_sum(dd, C, ws, labels, acc, mode):
+def _image_for(dd, k, mode, labels, image):
+    """The image an assignment call streams: ``image`` = (tensor, kind) when
+    the caller owns one (the fit's label-sorted image), else the dataset's
+    cached image for the screen (k, mode) selects (labels needed: the
+    image screens write labels only)."""
+    if image is not None:
+        return image
+    if labels is None:
+        return None, 0
+    return dd.screen_image(k, mode)
+
+
+def partial_sum(dd, C, ws, labels, acc, mode, image=None):
     so = _lib.lib()
     k = C.shape[0]
     if dd.sparse:
@@ -244,13 +262,13 @@ def partial_sum(dd, C, ws, labels, acc, mode):
             ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(acc), stream_ptr()),
             "dkm_partial_sum_csr_f64")
         return
-    img, kind = dd.screen_image(k, mode) if labels is not None else (None, 0)
+    img, kind = _image_for(dd, k, mode, labels, image)
     if img is not None:
         fn = so.dkm_partial_sum_img_f32 if dd.dtype == np.float32 else \
             so.dkm_partial_sum_img_f64
-        _lib.check(fn(ptr(dd.X), ptr(img), kind, dd.n, dd.d, dd.X.stride(0),
-                      ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(acc), mode,
-                      stream_ptr()), "dkm_partial_sum_img")
+        _lib.check(fn(ptr(dd.X), ptr(img), kind, img.numel(), dd.n, dd.d,
+                      dd.X.stride(0), ptr(C), k, ws.p, ws.nbytes, ptr(labels),
+                      ptr(acc), mode, stream_ptr()), "dkm_partial_sum_img")
         return
     fn = so.dkm_partial_sum_f32 if dd.dtype == np.float32 else \
         so.dkm_partial_sum_f64
@@ -259,7 +277,7 @@ def partial_sum(dd, C, ws, labels, acc, mode):
                "dkm_partial_sum")
 
 
-def assign_delta(dd, C, ws, labels, delta, mode):
+def assign_delta(dd, C, ws, labels, delta, mode, image=None):
     """Incremental assignment: labels in/out, delta +=."""
     so = _lib.lib()
     k = C.shape[0]
@@ -269,13 +287,13 @@ def assign_delta(dd, C, ws, labels, delta, mode):
             ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(delta),
             stream_ptr()), "dkm_assign_delta_csr_f64")
         return
-    img, kind = dd.screen_image(k, mode)
+    img, kind = _image_for(dd, k, mode, labels, image)
     if img is not None:
         fn = so.dkm_assign_delta_img_f32 if dd.dtype == np.float32 else \
             so.dkm_assign_delta_img_f64
-        _lib.check(fn(ptr(dd.X), ptr(img), kind, dd.n, dd.d, dd.X.stride(0),
-                      ptr(C), k, ws.p, ws.nbytes, ptr(labels), ptr(delta),
-                      mode, stream_ptr()), "dkm_assign_delta_img")
+        _lib.check(fn(ptr(dd.X), ptr(img), kind, img.numel(), dd.n, dd.d,
+                      dd.X.stride(0), ptr(C), k, ws.p, ws.nbytes, ptr(labels),
+                      ptr(delta), mode, stream_ptr()), "dkm_assign_delta_img")
         return
     fn = so.dkm_assign_delta_f32 if dd.dtype == np.float32 else \
         so.dkm_assign_delta_f64
@@ -284,40 +302,41 @@ def assign_delta(dd, C, ws, labels, delta, mode):
                "dkm_assign_delta")
 
 
-def prune_supported(dd, k):
+def sorted_image_ok(dd, k):
+    """Does the fit's auto mode on (k, d) run the single-product screen that
+    takes a label-sorted image (dkm_x_image_sorted_ok)?"""
+    if dd.sparse or dd.n == 0 or not X_IMAGE:
+        return False
     so = _lib.lib()
-    return (not dd.sparse and dd.n > 0 and
-            bool(so.dkm_prune_supported(int(k), dd.d)))
+    return (int(so.dkm_x_image_kind(int(k), dd.d, _lib.MODE_AUTO)) ==
+            _lib.IMAGE_SINGLE and bool(so.dkm_x_image_sorted_ok(int(k), dd.d)))
 
 
-class PruneState:
-    """Caller-owned state of dkm_assign_pruned_* (per-sample distance
-    bounds, active list, gather block) for one fit on one DeviceData."""
-
-    def __init__(self, dd, k):
-        t = torch()
-        so = _lib.lib()
-        self.nbytes = int(so.dkm_prune_state_bytes(dd.n, int(k), dd.d))
-        self.buf = t.empty(self.nbytes, dtype=t.uint8, device=dd.device)
-        self.valid = False       # bounds written by a previous call
-
-
-def assign_pruned(dd, C, C_prev, ws, labels, delta, st):
-    """dkm_assign_pruned_*: labels in/out, delta +=; returns the number of
-    samples screened (the others' labels are proven unchanged)."""
+def sorted_image(dd, labels, k, ws, old=None):
+    """dkm_x_image_sorted_*: the sample image with its rows grouped by
+    ``labels`` (a fit's current assignment), as (tensor, IMAGE_SORTED); the
+    buffer of ``old`` is reused.  (None, 0) when it would leave less than
+    4 GiB of HBM free or the workspace's label scratch is shorter than n.
+    The image carries a copy of the labels: pass it to every later call
+    that updates them (partial_sum / assign_delta ``image=``)."""
+    t = torch()
     so = _lib.lib()
-    k = C.shape[0]
-    img, kind = dd.screen_image(k, _lib.MODE_BF16)
-    fn = so.dkm_assign_pruned_f32 if dd.dtype == np.float32 else \
-        so.dkm_assign_pruned_f64
-    na = ctypes.c_int64(0)
-    _lib.check(fn(ptr(dd.X), ptr(img), kind, dd.n, dd.d, dd.X.stride(0),
-                  ptr(C),
-                  ptr(C_prev), k, ws.p, ws.nbytes, ptr(labels), ptr(delta),
-                  ptr(st.buf), st.nbytes, 0 if st.valid else 1,
-                  ctypes.byref(na), stream_ptr()), "dkm_assign_pruned")
-    st.valid = True
-    return int(na.value)
+    nb = int(so.dkm_x_image_bytes(dd.n, dd.d, _lib.IMAGE_SORTED))
+    if old is not None and old[0] is not None and old[0].numel() >= nb:
+        img = old[0]
+    else:
+        free = t.cuda.mem_get_info(dd.device)[0]
+        if nb == 0 or nb + _IMAGE_HEADROOM > free:
+            return None, 0
+        img = t.empty(nb, dtype=t.uint8, device=dd.device)
+    if int(so.dkm_workspace_bytes(int(k), dd.d, dd.n)) > ws.nbytes:
+        return None, 0
+    fn = so.dkm_x_image_sorted_f32 if dd.dtype == np.float32 else \
+        so.dkm_x_image_sorted_f64
+    _lib.check(fn(ptr(dd.X), dd.n, dd.d, dd.X.stride(0), ptr(labels), int(k),
+                  ws.p, ws.nbytes, ptr(img), nb, stream_ptr()),
+               "dkm_x_image_sorted")
+    return img, _lib.IMAGE_SORTED
 
 
 def label_sums(dd, ws, labels, acc, k):
@@ -386,3 +405,13 @@ def rechecked(ws):
     _lib.check(so.dkm_screen_stats(ws.p, ctypes.byref(out), stream_ptr()),
                "dkm_screen_stats")
     return int(out.value)
+
+
+def screen_counters(ws):
+    """(threshold-pass tiles, tiles it decided, centre blocks screened over
+    the label-sorted image) accumulated over the workspace's life."""
+    so = _lib.lib()
+    out = (ctypes.c_int64 * 3)()
+    _lib.check(so.dkm_screen_counters(ws.p, out, stream_ptr()),
+               "dkm_screen_counters")
+    return tuple(int(x) for x in out)

@@ -11,9 +11,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DKM_LIB", os.path.join(_HERE, "libdkm.so"))
 
 # constants mirrored from include/dkm.h
-ABI_VERSION = 1
+ABI_VERSION = 2
 MODE_AUTO, MODE_EXACT, MODE_SCREEN32, MODE_BF16X3, MODE_BF16 = 0, 1, 2, 3, 4
-IMAGE_NONE, IMAGE_SINGLE, IMAGE_SPLIT = 0, 1, 2
+MODE_MASK, MODE_NOHINT, MODE_B1 = 0xff, 0x100, 0x200
+IMAGE_NONE, IMAGE_SINGLE, IMAGE_SPLIT, IMAGE_SORTED = 0, 1, 2, 3
 SUMS_F64, SUMS_F32, SUMS_RECIP = 0, 1, 2
 PREP_CSR = 1
 COMM_ID_BYTES = 128
@@ -43,22 +44,19 @@ SIGNATURES = {
     "dkm_x_image_bytes": (_sz, [_i64, _i64, _i32]),
     "dkm_x_image_f64": (_i32, [_p, _i64, _i64, _i64, _i32, _p, _sz, _p]),
     "dkm_x_image_f32": (_i32, [_p, _i64, _i64, _i64, _i32, _p, _sz, _p]),
-    "dkm_partial_sum_img_f64": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p,
-                                       _i64, _p, _sz, _p, _p, _i32, _p]),
-    "dkm_partial_sum_img_f32": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p,
-                                       _i64, _p, _sz, _p, _p, _i32, _p]),
-    "dkm_assign_delta_img_f64": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p,
-                                        _i64, _p, _sz, _p, _p, _i32, _p]),
-    "dkm_assign_delta_img_f32": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p,
-                                        _i64, _p, _sz, _p, _p, _i32, _p]),
-    "dkm_prune_state_bytes": (_sz, [_i64, _i64, _i64]),
-    "dkm_prune_supported": (_i32, [_i64, _i64]),
-    "dkm_assign_pruned_f64": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p, _p,
-                                     _i64, _p, _sz, _p, _p, _p, _sz, _i32,
-                                     ctypes.POINTER(_i64), _p]),
-    "dkm_assign_pruned_f32": (_i32, [_p, _p, _i32, _i64, _i64, _i64, _p, _p,
-                                     _i64, _p, _sz, _p, _p, _p, _sz, _i32,
-                                     ctypes.POINTER(_i64), _p]),
+    "dkm_x_image_sorted_ok": (_i32, [_i64, _i64]),
+    "dkm_x_image_sorted_f64": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p,
+                                      _sz, _p, _sz, _p]),
+    "dkm_x_image_sorted_f32": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p,
+                                      _sz, _p, _sz, _p]),
+    "dkm_partial_sum_img_f64": (_i32, [_p, _p, _i32, _sz, _i64, _i64, _i64,
+                                       _p, _i64, _p, _sz, _p, _p, _i32, _p]),
+    "dkm_partial_sum_img_f32": (_i32, [_p, _p, _i32, _sz, _i64, _i64, _i64,
+                                       _p, _i64, _p, _sz, _p, _p, _i32, _p]),
+    "dkm_assign_delta_img_f64": (_i32, [_p, _p, _i32, _sz, _i64, _i64, _i64,
+                                        _p, _i64, _p, _sz, _p, _p, _i32, _p]),
+    "dkm_assign_delta_img_f32": (_i32, [_p, _p, _i32, _sz, _i64, _i64, _i64,
+                                        _p, _i64, _p, _sz, _p, _p, _i32, _p]),
     "dkm_label_sums_f64": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz,
                                   _p, _p]),
     "dkm_label_sums_f32": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _sz,
@@ -81,6 +79,7 @@ SIGNATURES = {
     "dkm_make_blobs_f64": (_i32, [_p, _i64, _i64, _i64, _i64, _u64, _f64,
                                   _f64, _p, _p]),
     "dkm_screen_stats": (_i32, [_p, ctypes.POINTER(_i64), _p]),
+    "dkm_screen_counters": (_i32, [_p, ctypes.POINTER(_i64), _p]),
     # distance-primitive reuse (kNN, DBSCAN epsilon query)
     "dkm_knn_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "dkm_knn_f64": (_i32, [_p, _i64, _i64, _p, _i64, _i64, _i64, _i64, _p,

@@ -157,14 +157,14 @@ class KMeans:
 # bit-identical to that last full recomputation.
 REFRESH = int(os.environ.get("DKM_REFRESH", "64"))
 
-# Bound-based skipping (dkm_assign_pruned_*, dkm_prune.hip): from the second
-# iteration on, samples whose distance bounds prove their label unchanged
-# are not screened.  Labels are identical either way.  Opt-in (DKM_PRUNE=1):
-# on the C3 shard the bf16 screen's bounds leave 12-39 % of the samples
-# active through iteration 10 (the fit's centres crowd), and the bounds
-# pass, gather and tier-2 re-reads made the iterations slower than
-# screening everything (profiles/r03/prune/).
-PRUNE = os.environ.get("DKM_PRUNE", "0") == "1"
+# The fit's label-sorted sample image (dkm_x_image_sorted_*, DESIGN.md
+# 3.11): built from the labels of iteration SORT_AT (the first assignment
+# against centres that are means of samples), it groups each 32-row tile
+# under one label so the single-product screen skips the centre blocks the
+# triangle inequality clears.  Labels are identical without it
+# (DKM_SORTED_IMAGE=0: A/B and parity runs).
+SORTED_IMAGE = os.environ.get("DKM_SORTED_IMAGE", "1") != "0"
+SORT_AT = 1
 
 
 class _Lloyd:
@@ -223,15 +223,11 @@ class _Lloyd:
         # every rank must refresh on the same iterations (their delta states
         # are summed): rank 0's setting wins
         self.refresh = _shard.broadcast_int(REFRESH, dd.device)
-        from .._device import prune_supported
-        self.pstate = None
-        self.C_prev = None
-        self.active = []          # samples screened per pruned iteration
-        if (PRUNE and mode in ("auto", "bf16") and
-                prune_supported(dd, k)):
-            from .._device import PruneState
-            self.pstate = PruneState(dd, k)
-            self.C_prev = t.empty_like(self.C)
+        from .._device import sorted_image_ok
+        # the label-sorted image: auto mode on the single-product shapes
+        self.sorting = (SORTED_IMAGE and mode == "auto" and
+                        sorted_image_ok(dd, k))
+        self.simg = None          # (tensor, IMAGE_SORTED) once built
 
     def prepare(self):
         """Per-iteration centre data + zeroed accumulator."""
@@ -240,43 +236,46 @@ class _Lloyd:
             prepare(self.C, self.ws, self.acc, csr=self.sparse)
 
     def _full(self):
-        return self.it == 0 or (self.it % self.refresh == 0 and self.dirty)
+        # iteration 1 recomputes too: its labels are the first against
+        # centres that are means of samples, and most samples move (a delta
+        # pass would add and subtract most rows: 2x a full pass at C3)
+        return self.it <= 1 or (self.it % self.refresh == 0 and self.dirty)
 
     def partial(self):
         """The hot kernel: fused assignment over all resident samples, full
         partial sums (dkm_partial_sum_*) or incremental (dkm_assign_delta_*).
         """
-        from .._device import assign_delta, partial_sum
+        from .._device import assign_delta, partial_sum, sorted_image
         if self.dd.n == 0:
             return
-        # "auto": the first iteration scores against the initial centres,
-        # where the single-product screen the library picks for large k x d
-        # would leave most samples undecided -- screen it with bf16x3
         mode = self.mode
+        image = None
         if mode == _lib.MODE_AUTO and self.it == 0:
+            # the first iteration scores against the initial centres, where
+            # the single-product screen the library picks for large k x d
+            # would leave most samples undecided -- screen it with bf16x3
             mode = _lib.MODE_BF16X3
+        elif self.sorting:
+            if self.it <= SORT_AT:
+                # the labels of the initial centres are poor hints (most
+                # samples move): the top-3 pass directly, and no image yet
+                # (X is converted in the screen; the sorted image is built
+                # from this iteration's labels)
+                mode |= _lib.MODE_NOHINT
+                image = (None, 0)
+            else:
+                image = self.simg or (None, 0)
         with self._on():
-            if self.pstate is not None and self.it > 0:
-                self._pruned()
-            elif self._full():
+            if self._full():
                 partial_sum(self.dd, self.C, self.ws, self.labels, self.acc,
-                            mode)
+                            mode, image=image)
             else:
                 assign_delta(self.dd, self.C, self.ws, self.labels, self.acc,
-                             mode)
-
-    def _pruned(self):
-        """Incremental assignment with bound-based skipping; on a refresh
-        iteration the sums are then recomputed from the labels."""
-        from .._device import assign_pruned, label_sums
-        na = assign_pruned(self.dd, self.C, self.C_prev, self.ws, self.labels,
-                           self.acc, self.pstate)
-        self.active.append(na)
-        self.C_prev.copy_(self.C)
-        if self._full():
-            self.acc.zero_()
-            label_sums(self.dd, self.ws, self.labels[:self.dd.n], self.acc,
-                       self.k)
+                             mode, image=image)
+            if self.sorting and self.it == SORT_AT:
+                simg = sorted_image(self.dd, self.labels[:self.dd.n], self.k,
+                                    self.ws)
+                self.simg = simg if simg[0] is not None else None
 
     def assign(self):
         self.prepare()
@@ -316,6 +315,13 @@ class _Lloyd:
 
     def criterion(self):
         return float(self.diff[0].item())
+
+    def screened_blocks(self):
+        """Diagnostics of the label-sorted image: (tiles threshold-screened,
+        centre blocks screened) accumulated over the workspace's life."""
+        from .._device import screen_counters
+        with self._on():
+            return screen_counters(self.ws)
 
     def rechecked(self):
         from .._device import rechecked

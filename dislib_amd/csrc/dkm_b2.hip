@@ -37,6 +37,16 @@
 // and -2c, the fp32 MFMA chain (now over |T| + sum |x c|, <= 2.04 mag), the
 // ŝ_p chain, and the few roundings of (acc + T) + |c|^2 -- each <= 2^-23 of
 // a magnitude <= 2.04 mag.  The top-3 fallback keeps b1's packed bound.
+//
+// Block skipping (the label-sorted image, IMG_SORTED).  The fit builds the
+// image once with its rows grouped by label (dkm_x_image_sorted_*), so a
+// 32-row tile almost always carries one hint p for all its rows.  With
+// u >= every row's reference distance to c_p (from s_hat_p and the bound)
+// and mind[p][cb] <= the distance from c_p to the nearest other centre of
+// block cb, a block with mind > 2u holds only centres strictly farther from
+// every row than c_p (triangle inequality, Elkan): it is not screened.  At
+// C3 most tiles then screen a third of the blocks.  The
+// labels never depend on the grouping, only the speed.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -59,29 +69,13 @@ constexpr int SB2 = DKM_AB_SB2;
 constexpr uint32_t PACK2 = 9, PACK2_MASK = (1u << PACK2) - 1;
 constexpr int B2_ENT = 3;    // kept (score, centre) per sample besides p
 constexpr int B2_RTHR = 4;   // over-full samples a wave tolerates per tile
-// bounds mode (B2View::bnd): the threshold is raised by M = min(B2_MU d_p^2,
-// mag) per row for a "near" test, so a row with no centre in (T, T + M]
-// gets a second-best lower bound M above its own distance (dkm_prune.hip)
-constexpr float B2_MU = 3.0f;
-constexpr int B2_NEAR = 0x10000;  // s_cnt flag: a centre within T + M
 // per-wave LDS scratch: -T[32], hint[32], count[32], |x|^2[32], the tile
 // transpose (32 rows x 16 bf16 features, 1 KB; the kept entries
 // [32][B2_ENT] reuse it after the tile's conversion), then 32 x nkw
 // own-mask words
 constexpr int B2_SCR_FIXED = 4 * 128 + 1024;
-// producer/consumer form (PC): B2_NLOAD loader waves (one per SIMD) stream
-// tiles through a ring of B2_S LDS slots (bf16 tile in the operand layout,
-// |x|^2, hints) to the consumer waves, which claim tiles in order from an
-// LDS counter.  Consumer scratch: -T, hints, counts, (|x|^2 unused), kept
-// entries, own masks.
-constexpr int B2_NLOAD = 4;
-constexpr int B2_S = 3;
-constexpr int B2_CSCR = 4 * 128 + 32 * B2_ENT * 8 + 128;  // + s_hat_p
-__host__ __device__ constexpr int b2_slot_bytes(int nks) {
-  return nks * 1024 + 256;
-}
-static_assert(32 * B2_ENT * 8 + 128 <= 1024,
-              "kept entries and s_hat_p fit the transpose");
+static_assert(32 * B2_ENT * 8 + 256 <= 1024,
+              "kept entries, s_hat_p and the sample ids fit the transpose");
 
 // v_min3 / v_min without fminf's NaN canonicalisation (inline asm: the
 // compiler would insert v_max_f32 x, x on every MFMA result)
@@ -132,46 +126,41 @@ struct B2View {
   int2 *tlist, *clist;
   int4 *nlist;
   int32_t *tcount, *ccount, *ncount;
-  // bounds mode: per row (upper bound on the distance to the final label,
-  // lower bound on every other centre's if that label is .w, else the
-  // third) -- see dkm_prune.hip; nullptr = off
-  float4 *bnd;
+  // block skipping (IMG_SORTED): mind[p * MIND_LD + cb] = a lower bound on
+  // min_{j in block cb, j != p} |c_p - c_j| (dkm_util.hip k_mind); nullptr
+  // = no skipping
+  const float *mind;
 };
 
-template <class TX, int NKS, bool W1, bool PC, bool IMG>
+// IMG: IMG_NONE (X converted in the kernel), IMG_SINGLE (the resident bf16
+// image, sample order) or IMG_SORTED (the same image with its rows grouped
+// by label: tile rows are samples perm[32 t + r], hints come from the image's
+// own label copy plab, and centre blocks are skipped by the triangle bound)
+template <class TX, int NKS, bool W1, int IMG>
 __global__ void __launch_bounds__(SB2)
     k_screen_b2(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
                 B2View v, int32_t *__restrict__ lab_out, int64_t base,
-                int delta, int hint, XImage img) {
+                int hint, XImage img) {
   typedef float f32x16 __attribute__((ext_vector_type(16)));
+  constexpr bool SORTED = IMG == IMG_SORTED;
   constexpr int GB = 1 << (PACK2 - 4);  // 32-centre blocks per top-3 group
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int nkb = (int)(kpad32(k) / 32);
   // W1: one own-mask word per column (k <= 1024), held in a register
   const int nkw = W1 ? 1 : (nkb + 31) >> 5;
   char *frag = (char *)smem;                                // nkb x NKS KB
-  // b1-order norms for the top-3 fallback (PC: read from ncn instead)
-  float *cn = (float *)(frag + (int64_t)nkb * NKS * 1024);
-  float *ncn = cn + (PC ? 0 : nkb * 32);                    // -|c|^2, plain
+  float *cn = (float *)(frag + (int64_t)nkb * NKS * 1024);  // b1 order norms
+  float *ncn = cn + nkb * 32;                               // -|c|^2, plain
   char *scr0 = (char *)(ncn + nkb * 32);
-  // PC: the ring, its flags, then the consumers' scratch
-  char *ring = scr0;
-  int *rflag = (int *)(ring + B2_S * b2_slot_bytes(NKS));  // full, freed, next
-  if (PC) scr0 = (char *)(rflag + 4 * B2_S);
   {
     const f32x4 *src = (const f32x4 *)v.b1frag;
     f32x4 *dst = (f32x4 *)frag;
     for (int e = threadIdx.x; e < nkb * NKS * 64; e += SB2) dst[e] = src[e];
     for (int e = threadIdx.x; e < nkb * 32; e += SB2) {
-      if (!PC) cn[e] = v.cn32f[e];
+      cn[e] = v.cn32f[e];
       // padding centres: -2^100 (never passes a sane threshold)
       ncn[e] = e < k ? -v.cn32[e] : -0x1.0p100f;
     }
-    if (PC && threadIdx.x < B2_S) {
-      rflag[threadIdx.x] = -1;                      // full: tile held
-      rflag[B2_S + threadIdx.x] = threadIdx.x - B2_S;  // freed: last read
-    }
-    if (PC && threadIdx.x == 0) rflag[2 * B2_S] = 0;  // next tile to claim
   }
   const float cm =
       (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
@@ -181,7 +170,8 @@ __global__ void __launch_bounds__(SB2)
   bk.k_mag = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(
       2.0f * (2.0f * rel + 0x1.0p-23f * (float)(1u << PACK2)) * 1.0001f)));
   // threshold pass: no packing, the chain over |T| + sum |x c| (see top)
-  // (the chain starts from -(T + M), M <= mag: magnitudes <= 3.04 mag)
+  // (the chain's magnitudes stay <= 3.04 mag: the bound keeps the margin of
+  // the earlier raised-threshold form)
   const float relt = 1.02f * 0x1.0p-8f + (48.0f * NKS + 32.0f) * 0x1.0p-23f;
   BoundK bkt = bk;
   bkt.k_mag = __int_as_float(__builtin_amdgcn_readfirstlane(
@@ -192,39 +182,23 @@ __global__ void __launch_bounds__(SB2)
 
   const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#ifndef DKM_AB_B2_STAGGER
-#define DKM_AB_B2_STAGGER 0
-#endif
-  // A/B: de-phase the waves sharing a SIMD (waves s, s + 4, s + 8): wave
-  // slot j starts j x DKM_AB_B2_STAGGER x 64 cycles late
-  if (DKM_AB_B2_STAGGER) {
-    for (int t = 0; t < (wid >> 2); ++t)
-      __builtin_amdgcn_s_sleep(DKM_AB_B2_STAGGER);
-  }
-  constexpr int NW = PC ? SB2 / 64 - B2_NLOAD : SB2 / 64;  // screening waves
-  const int cw = PC ? wid - B2_NLOAD : wid;  // screening wave index
-  const int64_t wv = (int64_t)blockIdx.x * NW + cw;
-  const int64_t step = (int64_t)gridDim.x * (SB2 / 64) * 32;
-  // PC: this workgroup's tiles are blockIdx.x + j gridDim.x, j < J
-  const int64_t ntiles = (n - base + 31) / 32;
-  const int64_t J = ntiles > blockIdx.x
-                        ? (ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x
-                        : 0;
-  char *scr = scr0 + (int64_t)(PC ? cw : wid) *
-                         ((PC ? B2_CSCR : B2_SCR_FIXED) + 128 * nkw);
+  constexpr int NW = SB2 / 64;  // screening waves per block
+  const int64_t wv = (int64_t)blockIdx.x * NW + wid;
+  const int64_t step = (int64_t)gridDim.x * NW * 32;
+  char *scr = scr0 + (int64_t)wid * (B2_SCR_FIXED + 128 * nkw);
   float *s_tn = (float *)scr;              // -T per sample
   int *s_hp = (int *)(scr + 128);          // hint per sample (-1: none)
   int *s_cnt = (int *)(scr + 256);         // kept entries appended
   float *s_xx = (float *)(scr + 384);      // |x|^2 per sample
-  float *s_m = s_xx;                        // M per sample, in process()
   // s_hat_p per sample, through the block loop (in registers it was one
   // VGPR too many: a spill reload whose vmcnt(0) waited for the prefetch);
   // the free tail of the transpose area, past the kept entries
   float *s_sp = (float *)(scr + 512 + 32 * B2_ENT * 8);
+  // SORTED: the rows' sample indices through the block loop (same reason)
+  int *s_sid = (int *)(scr + 512 + 32 * B2_ENT * 8 + 128);
   char *s_tx = scr + 512;                   // one K-step of the tile, bf16
   int2 *s_ent = (int2 *)(scr + 512);       // (score bits, centre), later
-  uint32_t *s_om =
-      (uint32_t *)(scr + (PC ? B2_CSCR : B2_SCR_FIXED));  // [word][column]
+  uint32_t *s_om = (uint32_t *)(scr + B2_SCR_FIXED);  // [word][column]
   int2 *wl = v.tlist + wv * TL_CAP;  // >= 3 candidates
   int2 *cl = v.clist + wv * B1_CAP;  // 2 candidates
   int4 *nl = v.nlist + wv * B1_NCAP; // 3..6 candidates
@@ -232,6 +206,7 @@ __global__ void __launch_bounds__(SB2)
   const bool listing = wv < TL_SEGS && wv < B1_SEGS;
   int tl_cnt = 0, cl_cnt = 0, tl_over = 0;
   uint32_t t_tiles = 0, t_done = 0;  // threshold passes run / accepted
+  uint32_t t_blocks = 0;             // centre blocks screened (SORTED)
 
   // ---- tile loads: whole 128-B lines per wave-instruction ----------------
   // A lane's MFMA operand is 8 features of ITS sample, so loading it
@@ -265,7 +240,7 @@ __global__ void __launch_bounds__(SB2)
         (void *)(X + std::min(s0, n) * ldx), 0,
         (int)std::min<int64_t>(rows * ldx * (int64_t)sizeof(TX), 0x7fffffff),
         0x00020000);
-    if (delta || hint) {
+    if (hint) {
       const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
           (void *)(lab_out + std::min(s0, n)), 0,
           (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
@@ -301,15 +276,60 @@ __global__ void __launch_bounds__(SB2)
   }
   auto wofs_at = [&](int i) { return 32 * RI * i + wofs[EPL == 2 ? i & 1 : 0]; };
 
-  // A/B (-DDKM_AB_B2_PF=1, pair with -DDKM_AB_SB2=512): the next tile's
-  // loads are issued as soon as this one is converted
-#ifndef DKM_AB_B2_PF
-#define DKM_AB_B2_PF 0
+  // The image paths issue the next tile's loads after the block loop, not
+  // before the tile: its 20 registers are then not live across the loop,
+  // which kept the label-sorted variant from spilling (a spill reload's
+  // vmcnt wait also waited for the prefetch).  C3: 13.3 against 13.6 ms
+  // per step (profiles/r04/ab_latepf.txt); -DDKM_AB_B2_LATEPF=0 for A/B.
+#ifndef DKM_AB_B2_LATEPF
+#define DKM_AB_B2_LATEPF 1
 #endif
+  constexpr bool LATEPF = DKM_AB_B2_LATEPF && IMG != IMG_NONE;
+  int64_t pf_s0 = 0;     // LATEPF: the next tile to prefetch (>= n: none)
+  bool pf_done = true;
+  // the image paths' tile loads: each lane's operand is one 16-B piece of
+  // a 1 KB K-step block (whole lines), |x|^2 precomputed
+  auto load_img = [&](int64_t s0, bf16x8 (&dst)[NKS], float &xxd, int &pvd,
+                      int &sidd) {
+    const bf16x8 *src =
+        (const bf16x8 *)(img.tiles + (s0 >> 5) * (NKS * 512)) + lane;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      dst[ks] = __builtin_nontemporal_load(src + 64 * ks);
+    xxd = __builtin_nontemporal_load(img.xx + s0 + r);
+    if constexpr (SORTED) {
+      // the image holds whole tiles: rows past n carry perm = -1
+      sidd = __builtin_nontemporal_load(img.perm + s0 + r);
+      pvd = img.plab[s0 + r];
+    } else {
+      sidd = s0 + r < n ? (int)(s0 + r) : -1;
+      if (hint) {
+        const int64_t rows = std::max<int64_t>(0, n - s0);
+        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(lab_out + std::min(s0, n)), 0,
+            (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
+        pvd = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
+      }
+    }
+  };
+  bf16x8 xq[NKS];        // the next tile (image paths)
+  float xxq = 0.f;
+  int pq = -1, sq = -1;
+  auto late_prefetch = [&]() {
+    if (LATEPF && !pf_done) {
+      pf_done = true;
+      if (pf_s0 < n) load_img(pf_s0, xq, xxq, pq, sq);
+    }
+  };
+
   // ---- one tile: threshold pass (or top-3), decision, lists, labels ----
-  auto process = [&](int64_t s0, const bf16x8 (&xh)[NKS], float xx,
-                     int prv) {
-    const int64_t si = s0 + r;
+  // s0 = the tile's first row (image row for SORTED), sid = this lane's
+  // sample index (-1: a row past the data)
+  auto process = [&](int64_t s0, const bf16x8 (&xh)[NKS], float xx, int prv,
+                     int sid) {
+    // (prv, p, pok and sid are re-read from the wave's LDS scratch after
+    // the block loop: live across it they cost the registers that made the
+    // kernel spill)
     float xn;
     const float B2t = bound2_fast(bkt, xx, xn);
     const bool sane0 = (xn < 1e18f) & (xn * cm < 1e30f);
@@ -317,32 +337,25 @@ __global__ void __launch_bounds__(SB2)
     int i1 = 0, i2 = 0;
     uint32_t mpk0 = 0, mpk1 = 0, mpk2 = 0;  // many: the candidate set
     bool need3 = true;
-    // bounds mode: distance bounds from squared-score bounds, each with a
-    // 2^-20 relative margin (the fp32 evaluation, the sqrt, and the
-    // reference's own fp64 rounding); |x|^2 from fp32 within 2^-14.  Each
-    // path writes its row's bounds where it has them (nothing held live
-    // across the block loop: 6 such VGPRs made the kernel spill, and the
-    // spill reloads' vmcnt waits exposed the prefetched image's latency)
-    const bool bvalid = si < n && h == 0;
-    auto put_bounds = [&](float bu, float bl1, float bl0, int bi) {
-      if (bvalid)
-        v.bnd[si - base] = make_float4(bu, bl1, bl0, __int_as_float(bi));
-    };
-    auto ub_of = [](float q2) {
-      const float q = __builtin_sqrtf(fmaxf(q2, 0.f));
-      return q + q * 0x1.0p-20f;
-    };
-    auto lb_of = [](float q2) {
-      const float q = __builtin_sqrtf(fmaxf(q2, 0.f));
-      return q - q * 0x1.0p-20f;
-    };
     if (hint) {
-      const bool pok = prv >= 0 && prv < k && si < n;
-      const uint64_t bad = __ballot(!pok && si < n);
+      const bool pok = prv >= 0 && prv < k && sid >= 0;
+      const uint64_t bad = __ballot(!pok && sid >= 0);
       if (__popcll(bad) <= 2 * B2_RTHR) {
         const int p = pok ? prv : 0;
+        // SORTED: a tile whose rows all carry one hint p0 (most of them:
+        // the rows are grouped by label) skips every centre block the
+        // triangle inequality clears (below); its own block is empty
+        int p0 = 0;
+        bool uni = false;
+        float mnd = INFINITY;
+        if (SORTED && v.mind) {
+          p0 = __builtin_amdgcn_readfirstlane(prv);
+          uni = __ballot(sid >= 0 && prv != p0) == 0 && p0 >= 0 && p0 < k;
+          if (uni && lane < nkb) mnd = v.mind[(int64_t)p0 * MIND_LD + lane];
+        }
         // ---- own block: columns = the tile's hinted centres p_c ----------
-        f32x16 dn;
+        f32x16 dn = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
+                           0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         float dg = 0.f;
         {
           bf16x8 of[NKS];
@@ -351,12 +364,12 @@ __global__ void __launch_bounds__(SB2)
             of[ks] = *(const bf16x8 *)(frag + ((int64_t)(p >> 5) * NKS + ks) *
                                                   1024 +
                                        ((p & 31) + 32 * h) * 16);
-          dn = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
-                      0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          if (!uni) {
 #pragma unroll
-          for (int ks = 0; ks < NKS; ++ks)
-            dn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[ks], of[ks], dn, 0,
-                                                         0, 0);
+            for (int ks = 0; ks < NKS; ++ks)
+              dn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[ks], of[ks], dn,
+                                                           0, 0, 0);
+          }
           // s_hat_p's product x_r . (-2 c_p) by VALU dot products: lane
           // (r, h) holds x_r's and c_p's features 16 ks + 8h .. + 7 (xh and
           // of), so 4 NKS v_dot2c_f32_bf16 and one cross-half add (exact
@@ -379,18 +392,38 @@ __global__ void __launch_bounds__(SB2)
         const float ncp = ncn[p];
         const float sp = dg - ncp;  // s_hat_p = |c_p|^2 + x.(-2 c_p)
         const float T = pok ? sp + B2t : -INFINITY;
-        float Mr = 0.f;  // bounds mode: the near-test margin of row r
-        if (v.bnd && pok) {
-          const float magr = fmaf(xn, bkt.two_cm, bkt.cm2);
-          Mr = fminf(B2_MU * fmaxf(xx + sp, 0.f), magr);
+        // ---- SORTED: the centre blocks this tile must screen -------------
+        // Every row r has hint p0.  u_r bounds the reference distance
+        // |x_r - c_p0| from above: D^2 <= |x|^2 + s_hat_p + B2t / 2 (the
+        // screen bound), with 2^-16 on the fp32 |x|^2 and 2^-20 on the
+        // root.  A block cb with mind[p0][cb] > 2 max_r u_r holds only
+        // centres j with |x_r - c_j| >= |c_p0 - c_j| - |x_r - c_p0| >
+        // |x_r - c_p0| for every row -- strictly farther than the hint, so
+        // they can neither win nor tie (the margins cover the reference's
+        // own fp64 rounding of both distances).  Rows that are not sane go
+        // to the exact re-check whatever the blocks, so they do not count.
+        uint64_t bmask = 0;
+        if (SORTED) {
+          if (uni) {
+            float u = 0.f;
+            if (sid >= 0 && sane0) {
+              const float u2 = fmaf(xx, 1.0f + 0x1.0p-16f, sp + B2t);
+              u = __builtin_sqrtf(fmaxf(u2, 0.f)) * (1.0f + 0x1.0p-20f);
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1)
+              u = fmaxf(u, __shfl_xor(u, off, 64));
+            bmask = __ballot(lane < nkb && !(mnd > 2.0f * u));
+          } else {
+            bmask = nkb >= 64 ? ~0ull : ((1ull << nkb) - 1);
+          }
         }
         // ---- per-wave scratch: -T, hints, counts, own masks --------------
         wave_sync();
         if (h == 0) {
-          s_tn[r] = -(T + Mr);
+          s_tn[r] = -T;
           s_hp[r] = pok ? p : -1;
           s_cnt[r] = 0;
-          s_m[r] = Mr;
           s_sp[r] = sp;
         }
         for (int w = lane; w < 32 * nkw; w += 64) s_om[w] = 0u;
@@ -422,22 +455,14 @@ __global__ void __launch_bounds__(SB2)
           pg[4 * q + 3] = p4.w;
         }
         const uint32_t om0 = s_om[r];
-        // bounds mode: kept iff within T (the score + M test passed too);
-        // within (T, T + M] only flags the row as near
-        auto keep = [&](int row, float a, float t) {
-          const bool k2 = a + s_m[row] <= t;
-          if (!k2) atomicOr(&s_cnt[row], B2_NEAR);
-          return k2;
-        };
         auto push = [&](int row, float s, int j) {
-          // (the count is the low half: the near flag may be set)
-          const int slot = atomicAdd(&s_cnt[row], 1) & (B2_NEAR - 1);
+          const int slot = atomicAdd(&s_cnt[row], 1);
           if (slot < B2_ENT)
             s_ent[row * B2_ENT + slot] = make_int2(__float_as_int(s), j);
         };
         // own block: pairs (row, p) with p != p_row; the column of a centre
         // hinted by several samples is tested once (dup)
-        {
+        if (!uni) {
           float m = INFINITY;
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
@@ -449,11 +474,11 @@ __global__ void __launch_bounds__(SB2)
             for (int g = 0; g < 16; ++g)
               if (pg[g] != p && dn[g] + cin[g] <= ncp) {
                 const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
-                if (keep(row, dn[g] + cin[g], ncp)) push(row, dn[g] - ncp, p);
+                push(row, dn[g] - ncp, p);
               }
           }
         }
-        // ---- all centre blocks: lane = centre, registers = samples -------
+        // ---- centre blocks: lane = centre, registers = samples -----------
         auto rd_f = [&](int cb, bf16x8 (&f)[NKS]) {
 #pragma unroll
           for (int ks = 0; ks < NKS; ++ks)
@@ -494,12 +519,73 @@ __global__ void __launch_bounds__(SB2)
             for (int g = 0; g < 16; ++g)
               if (acc[g] <= thr) {
                 const int row = (g & 3) + 8 * (g >> 2) + 4 * h;
-                if (keep(row, acc[g], thr))
-                  push(row, (acc[g] - cin[g]) - nc, j);
+                push(row, (acc[g] - cin[g]) - nc, j);
               }
           }
         };
-        if (DKM_AB_B2_PROBE != 1) {
+        if (SORTED && DKM_AB_B2_PROBE != 1) {
+          // the blocks of bmask (wave-uniform), in the dense loop's
+          // software pipeline with c0..c3 = the next set bits in place of
+          // cb .. cb + 3
+          f32x16 acc_a, acc_b;
+          bf16x8 fa[NKS], fb[NKS];
+          float na, nb = 0.f, ta, tb;
+          bool ga, gb;
+          uint64_t m = bmask;
+          auto pop = [&]() -> int {
+            const int c = m ? __builtin_ctzll(m) : 0;
+            m &= m - 1;
+            return c;
+          };
+          int left = __popcll(bmask);
+          t_blocks += (uint32_t)left;
+          if (left > 0) {
+            int c0 = pop(), c1 = pop(), c2 = pop(), c3 = pop();
+            rd_f(c0, fa);
+            na = rd_n(c0);
+            mm(fa, acc_a);  // chain c0
+            if (left > 1) {
+              rd_f(c1, fb);
+              nb = rd_n(c1);
+            }
+            for (; left > 3; left -= 2) {
+              mm(fb, acc_b);  // chain c1
+              rd_f(c2, fa);
+              test(c0, acc_a, na, ta, ga);
+              append(c0, acc_a, ta, na, ga);
+              na = rd_n(c2);
+              mm(fa, acc_a);  // chain c2
+              rd_f(c3, fb);
+              test(c1, acc_b, nb, tb, gb);
+              append(c1, acc_b, tb, nb, gb);
+              nb = rd_n(c3);
+              c0 = c2;
+              c1 = c3;
+              c2 = pop();
+              c3 = pop();
+            }
+            // tail: 1, 2 or 3 blocks left (chain c0 issued, c1 read)
+            if (left > 1) {
+              mm(fb, acc_b);  // chain c1
+              if (left > 2) rd_f(c2, fa);
+              test(c0, acc_a, na, ta, ga);
+              append(c0, acc_a, ta, na, ga);
+              if (left > 2) {
+                na = rd_n(c2);
+                mm(fa, acc_a);  // chain c2
+              }
+              test(c1, acc_b, nb, tb, gb);
+              append(c1, acc_b, tb, nb, gb);
+              if (left > 2) {
+                test(c2, acc_a, na, ta, ga);
+                append(c2, acc_a, ta, na, ga);
+              }
+            } else {
+              test(c0, acc_a, na, ta, ga);
+              append(c0, acc_a, ta, na, ga);
+            }
+          }
+        } else if (DKM_AB_B2_PROBE != 1) {
           // software pipeline, one block deep: block t's chain is issued
           // before block t - 1 is tested (the test VALU overlaps the MFMA
           // chain instead of waiting for its own block's results), and the
@@ -550,19 +636,24 @@ __global__ void __launch_bounds__(SB2)
             append(cb, acc_a, ta, na, ga);
           }
         }
+        late_prefetch();
         // ---- decision over the hint and the kept entries ------------------
         wave_sync();
-        const int craw = s_cnt[r];
-        const int cnt = craw & (B2_NEAR - 1);
-        const bool nearr = craw >= B2_NEAR;
+        const int cnt = s_cnt[r];
+        // the hint as the scratch holds it: p when usable, else -1 (a row
+        // without a usable hint is `over`, so nothing below needs its
+        // incoming label)
+        prv = s_hp[(int)opaque_u32((uint32_t)r)];
+        const bool pokd = prv >= 0;
+        const int pd = pokd ? prv : 0;
         float sv[B2_ENT + 1];
         int cv[B2_ENT + 1];
         bool ok[B2_ENT + 1];
         // s_hat_p and T again (the same fp32 operation: the same bits)
         const float sp2 = s_sp[r];
-        const float T2 = pok ? sp2 + B2t : -INFINITY;
+        const float T2 = pokd ? sp2 + B2t : -INFINITY;
         sv[0] = sp2;
-        cv[0] = p;
+        cv[0] = pd;
         ok[0] = true;
 #pragma unroll
         for (int e = 0; e < B2_ENT; ++e) {
@@ -572,7 +663,7 @@ __global__ void __launch_bounds__(SB2)
           // (an index outside [0, k) never reaches the candidate kernels)
           ok[e + 1] = e < cnt && (unsigned)en.y < (unsigned)k;
         }
-        const bool over = cnt > B2_ENT || !pok || !sane0 || !(T2 < 1e30f);
+        const bool over = cnt > B2_ENT || !pokd || !sane0 || !(T2 < 1e30f);
         float bs = INFINITY;
         int bc = 0x7fffffff;
 #pragma unroll
@@ -596,7 +687,7 @@ __global__ void __launch_bounds__(SB2)
             ++namb;
             other = cv[e] != bc ? cv[e] : other;
           }
-        const uint64_t mo = __ballot(over && si < n && h == 0);
+        const uint64_t mo = __ballot(over && sid >= 0 && h == 0);
         ++t_tiles;
         if (__popcll(mo) <= B2_RTHR) {
           ++t_done;
@@ -609,45 +700,17 @@ __global__ void __launch_bounds__(SB2)
           mpk0 = pk[0];
           mpk1 = pk[1];
           mpk2 = pk[2];
-          if (v.bnd) {
-            // every centre outside the kept set K = {p} + entries has
-            // s_j > s_hat_p + B2t / 2 (+ M unless the row is near); inside
-            // K, s_j >= its score - B2t.  The final label is bc unless the
-            // exact re-check picks another member of K.
-            float m2 = INFINITY;
-#pragma unroll
-            for (int e = 0; e <= B2_ENT; ++e)
-              if (ok[e] && !(sv[e] == bs && cv[e] == bc)) m2 = fminf(m2, sv[e]);
-            const float Mr2 = s_m[r];
-            const float base = sp2 + 0.25f * B2t + (nearr ? 0.f : 0.99f * Mr2);
-            const float xxh = xx * (1.0f + 0x1.0p-14f),
-                        xxl = xx * (1.0f - 0x1.0p-14f);
-            if (over)
-              put_bounds(INFINITY, -INFINITY, -INFINITY, 0);
-            else
-              put_bounds(ub_of(xxh + bs + B2t),
-                         lb_of(xxl + fminf(base, m2 - B2t)),
-                         lb_of(xxl + fminf(base, bs - B2t)), bc);
-          }
         }
       }
     }
     if (need3) {
+      late_prefetch();
       // ---- top-3 pass (no usable hint): b1's layout, centres on the rows --
       auto chain = [&](int cb, f32x16 &accv) {
-        if constexpr (PC) {
-          // register g = centre cb*32 + (g & 3) + 8 (g >> 2) + 4h: four
-          // runs of 4 in the plain -|c|^2 table
-          const f32x4 *c4p = (const f32x4 *)(ncn + cb * 32 + 4 * h);
-          const f32x4 c0 = c4p[0], c1 = c4p[2], c2 = c4p[4], c3 = c4p[6];
-          accv = -f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
-                         c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-        } else {
-          const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
-          const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
-          accv = f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
-                        c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-        }
+        const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
+        const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
+        accv = f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                      c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
           const bf16x8 ah =
@@ -735,23 +798,12 @@ __global__ void __launch_bounds__(SB2)
       }
       const bool sane = sane0 & (r1 < 1e30f);
       const float B2 = bound2_fast(bk, xx, xn);
-      if (v.bnd) {
-        // packed scores: within B2 / 2 each (the packing included)
-        const float xxh = xx * (1.0f + 0x1.0p-14f),
-                    xxl = xx * (1.0f - 0x1.0p-14f);
-        if (sane)
-          put_bounds(ub_of(xxh + r1 + B2), lb_of(xxl + r2 - B2),
-                     lb_of(xxl + r1 - B2), ii1);
-        else
-          put_bounds(INFINITY, -INFINITY, -INFINITY, 0);
-      }
       unique = sane & (r2 - r1 > B2);
       two = sane & !unique & (r3 - r1 > B2);
       i1 = ii1;
       i2 = ii2;
     }
-    const bool valid = si < n && h == 0;
-    const int prev = delta ? prv : -1;
+    const bool valid = sid >= 0 && h == 0;
     // 3..6 candidates of the threshold pass -> the N-candidate list
     bool nlisted = false;
     {
@@ -760,7 +812,7 @@ __global__ void __launch_bounds__(SB2)
       if (addn && listing && nl_cnt + addn <= B1_NCAP) {
         if (valid && many)
           nl[nl_cnt + lane_prefix(mn)] =
-              make_int4((int)(si - base), (int)mpk0, (int)mpk1, (int)mpk2);
+              make_int4((int)(sid - base), (int)mpk0, (int)mpk1, (int)mpk2);
         nl_cnt += addn;
         nlisted = many;
       }
@@ -772,167 +824,54 @@ __global__ void __launch_bounds__(SB2)
     if (listing && cl_cnt + addc <= B1_CAP) {
       if (valid && two)
         cl[cl_cnt + lane_prefix(mc)] =
-            make_int2((int)(si - base), i1 | (i2 << 16));
+            make_int2((int)(sid - base), i1 | (i2 << 16));
       cl_cnt += addc;
     } else {
       tl_over += addc;
     }
     if (listing && tl_cnt + addt <= TL_CAP) {
       if (valid && !unique && !two && !nlisted)
-        wl[tl_cnt + lane_prefix(mt)] = make_int2((int)(si - base), prev);
+        wl[tl_cnt + lane_prefix(mt)] = make_int2((int)(sid - base), -1);
       tl_cnt += addt;
     } else {
       tl_over += addt;
     }
     // a label equal to the incoming one (the hint) needs no store; an
     // N-listed sample keeps it until k_candn writes the winner.  A sample
-    // that overflowed a list keeps -(prev + 2): the label scan finds it.
-    if (valid && !nlisted && !(unique && i1 == (hint ? prv : prev)))
-      lab_out[si] = unique ? i1 : -(prev + 2);
+    // that overflowed a list keeps -1 (-(prev + 2), no previous label in
+    // this labels-only pass): the label scan finds it.  SORTED: the image's
+    // label copy follows, -1 where a re-check kernel writes the label
+    // (k_plab_sync fetches it afterwards).
+    if (valid) {
+      const bool same = unique && i1 == prv && (hint || SORTED);
+      if (!nlisted && !same) lab_out[sid] = unique ? i1 : -1;
+      if (SORTED && !same) img.plab[s0 + r] = unique ? i1 : -1;
+    }
   };
 
-  if constexpr (PC) {
-    // ---- producer/consumer: loaders stream tiles into the ring ----------
-    int *full = rflag, *freed = rflag + B2_S, *next = rflag + 2 * B2_S;
-    auto tile_s0 = [&](int64_t j) {
-      return base + ((int64_t)blockIdx.x + j * gridDim.x) * 32;
-    };
-    // bounded spin on an LDS word (a correct ring never reaches the bound;
-    // past it the wave stops waiting -- wrong labels, never a hung GPU)
-    auto wait_eq = [&](int *p, int want) {
-      for (int it = 0; it < (1 << 22); ++it) {
-        if (__hip_atomic_load(p, __ATOMIC_ACQUIRE,
-                              __HIP_MEMORY_SCOPE_WORKGROUP) == want)
-          return;
-        __builtin_amdgcn_s_sleep(1);
-      }
-    };
-    if (wid < B2_NLOAD) {
-      // loader: its tiles j = wid, wid + NLOAD, ... with the next one's
-      // loads in flight while this one is converted into its slot
-      tx4 rawb[NKS][IC];
-      int pvb = -1;
-      auto publish = [&](int64_t j, const tx4 (&rw)[NKS][IC], int hp) {
-        const int sl = (int)(j % B2_S);
-        char *slot = ring + sl * b2_slot_bytes(NKS);
-        float *sxx = (float *)(slot + NKS * 1024);
-        int *shp = (int *)(slot + NKS * 1024 + 128);
-        wait_eq(&freed[sl], (int)j - B2_S);  // the slot's previous tile read
-        float xp[IC];
-#pragma unroll
-        for (int i = 0; i < IC; ++i) xp[i] = 0.f;
-        const int lim = d == 16 * NKS
-                            ? 0x7fffffff
-                            : (int)opaque_u32((uint32_t)(d - EPL * lpos));
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          char *stx = slot + ks * 1024;
-#pragma unroll
-          for (int i = 0; i < IC; ++i) {
-            float xf[EPL];
-#pragma unroll
-            for (int e = 0; e < EPL; ++e) {
-              const float x = (float)rw[ks][i][e];
-              xf[e] = 16 * ks + e < lim ? x : 0.f;
-              xp[i] = fmaf(xf[e], xf[e], xp[i]);
-            }
-            if constexpr (EPL == 2) {
-              *(bf16x2 *)(stx + wofs_at(i)) =
-                  __builtin_convertvector(f32x2{xf[0], xf[1]}, bf16x2);
-            } else {
-              typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-              const bf16x2 a2 =
-                  __builtin_convertvector(f32x2{xf[0], xf[1]}, bf16x2);
-              const bf16x2 b2 =
-                  __builtin_convertvector(f32x2{xf[2], xf[3]}, bf16x2);
-              *(bf16x4 *)(stx + wofs_at(i)) = bf16x4{a2[0], a2[1], b2[0], b2[1]};
-            }
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < IC; ++i) {
-#pragma unroll
-          for (int m = 1; m < LR; m <<= 1) xp[i] += __shfl_xor(xp[i], m, 64);
-          if (lpos == 0) sxx[RI * i + lrow] = xp[i];
-        }
-        if (h == 0) shp[r] = hp;
-        // release: the slot's writes are complete before `full` says so
-        if (lane == 0)
-          __hip_atomic_store(&full[sl], (int)j, __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-      };
-      // two register sets, A = raw and B = rawb, alternating (unrolled:
-      // no runtime-indexed register arrays); publishing A waits only for
-      // A's loads, B's stay in flight
-      int64_t j = wid;
-      if (j < J) load_into(tile_s0(j), raw, pv);
-      for (; j < J; j += 2 * B2_NLOAD) {
-        if (j + B2_NLOAD < J) load_into(tile_s0(j + B2_NLOAD), rawb, pvb);
-        publish(j, raw, pv);
-        if (j + B2_NLOAD >= J) break;
-        if (j + 2 * B2_NLOAD < J) load_into(tile_s0(j + 2 * B2_NLOAD), raw, pv);
-        publish(j + B2_NLOAD, rawb, pvb);
-      }
-      return;
-    }
-    (void)img;
-    // consumer: claim tiles in order; read the slot into registers, free it
-    for (;;) {
-      int j = 0;
-      if (lane == 0) j = atomicAdd(next, 1);
-      j = __builtin_amdgcn_readfirstlane(j);
-      if (j >= J) break;
-      const int sl = j % B2_S;
-      const char *slot = ring + sl * b2_slot_bytes(NKS);
-      wait_eq(&full[sl], j);
-      bf16x8 xh[NKS];
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-        xh[ks] = *(const bf16x8 *)(slot + ks * 1024 + tx_addr(r, h));
-      const float xx = ((const float *)(slot + NKS * 1024))[r];
-      const int prv = ((const int *)(slot + NKS * 1024 + 128))[r];
-      if (lane == 0)
-        __hip_atomic_store(&freed[sl], j, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
-      process(tile_s0(j), xh, xx, prv);
-    }
-  } else if constexpr (IMG) {
-    // ---- sample image: each lane's operand is one 16-B piece of a 1 KB
-    // K-step block (whole lines), |x|^2 precomputed; the next tile's
-    // loads are in flight while this one is screened
-    auto load_img = [&](int64_t s0, bf16x8 (&dst)[NKS], float &xxd, int &pvd) {
-      const bf16x8 *src =
-          (const bf16x8 *)(img.tiles + (s0 >> 5) * (NKS * 512)) + lane;
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-        dst[ks] = __builtin_nontemporal_load(src + 64 * ks);
-      xxd = __builtin_nontemporal_load(img.xx + s0 + r);
-      if (delta || hint) {
-        const int64_t rows = std::max<int64_t>(0, n - s0);
-        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(lab_out + std::min(s0, n)), 0,
-            (int)std::min<int64_t>(rows * 4, 0x7fffffff), 0x00020000);
-        pvd = (int)__builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0);
-      }
-    };
+  if constexpr (IMG != IMG_NONE) {
+    // ---- sample image: the next tile's loads are in flight while this one
+    // is screened (LATEPF: issued from process() after the block loop)
     int64_t s0 = base + wv * 32;
-    bf16x8 xq[NKS];
-    float xxq = 0.f;
-    int pq = -1;
-    if (s0 < n) load_img(s0, xq, xxq, pq);
+    if (s0 < n) load_img(s0, xq, xxq, pq, sq);
     for (; s0 < n; s0 += step) {
       bf16x8 xh[NKS];
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) xh[ks] = xq[ks];
       const float xx = xxq;
-      const int prv = pq;
-      if (s0 + step < n) load_img(s0 + step, xq, xxq, pq);
-      process(s0, xh, xx, prv);
+      const int prv = pq, sid = sq;
+      if (LATEPF) {
+        pf_s0 = s0 + step;
+        pf_done = false;
+      } else if (s0 + step < n) {
+        load_img(s0 + step, xq, xxq, pq, sq);
+      }
+      process(s0, xh, xx, prv, sid);
+      late_prefetch();
     }
   } else {
-  if (DKM_AB_B2_PF && base + wv * 32 < n) load_tile(base + wv * 32);
   for (int64_t s0 = base + wv * 32; s0 < n; s0 += step) {
-    if (!DKM_AB_B2_PF) load_tile(s0);
+    load_tile(s0);
     bf16x8 xh[NKS];
     float xp[IC];  // |x|^2 partials of rows RI i + lrow
 #pragma unroll
@@ -976,11 +915,9 @@ __global__ void __launch_bounds__(SB2)
     }
     wave_sync();
     const float xx = s_xx[r];
-    const int prv = pv;
-    if (DKM_AB_B2_PF && s0 + step < n) load_tile(s0 + step);
-    process(s0, xh, xx, prv);
+    process(s0, xh, xx, pv, s0 + r < n ? (int)(s0 + r) : -1);
   }
-  }  // !PC
+  }  // IMG_NONE
   if (lane == 0 && listing) {
     v.tcount[wv] = tl_cnt;
     v.ccount[wv] = cl_cnt;
@@ -991,6 +928,9 @@ __global__ void __launch_bounds__(SB2)
               (unsigned long long)t_tiles);
     atomicAdd((unsigned long long *)&v.hdr->reserved[1],
               (unsigned long long)t_done);
+    if (SORTED)
+      atomicAdd((unsigned long long *)&v.hdr->reserved[2],
+                (unsigned long long)t_blocks);
   }
   if (lane == 0 && tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
 }
@@ -1001,33 +941,8 @@ size_t b2_lds_bytes(int64_t k, int64_t d) {
          (size_t)(SB2 / 64) * (B2_SCR_FIXED + 128 * nkw);
 }
 
-// the producer/consumer form's LDS image (no b1-order norm copy)
-static size_t b2pc_lds_bytes(int64_t k, int64_t d) {
-  const int64_t nkb = kpad32(k) / 32, nkw = (nkb + 31) / 32;
-  const int nks = (int)(dpad16(d) / 16);
-  return (size_t)nkb * nks * 1024 + (size_t)nkb * 128 +
-         (size_t)B2_S * b2_slot_bytes(nks) + 16 * B2_S +
-         (size_t)(SB2 / 64 - B2_NLOAD) * (B2_CSCR + 128 * nkw);
-}
-
-// DKM_B1_LEGACY=1 runs k_screen_b1 instead (A/B and its parity tests); read
-// per launch so that one process can run both
+// A/B timing probe builds (variants_b2.sh) report themselves
 int b2_probe() { return DKM_AB_B2_PROBE; }
-
-bool b2_enabled() {
-  const char *e = getenv("DKM_B1_LEGACY");
-  return !(e && *e && *e != '0');
-}
-
-// DKM_B2_PC=1: the producer/consumer form (4 loader waves feeding 8
-// screening waves through an LDS ring).  Off by default: at C3 it ran
-// 39.8 ms per launch against 24.0 ms for every wave loading its own tiles
-// (profiles/r03/b2/r03g_*): the loaders' two register tiles spill, and 8
-// screening waves hide less than 12.  Read per launch.
-static bool b2pc_enabled() {
-  const char *e = getenv("DKM_B2_PC");
-  return e && *e == '1';
-}
 
 // ---- the sample image (dkm_x_image_*) ----------------------------------
 static int64_t img_tile_bytes(int64_t d, int kind) {
@@ -1036,15 +951,23 @@ static int64_t img_tile_bytes(int64_t d, int kind) {
 
 size_t x_image_bytes(int64_t n, int64_t d, int kind) {
   const int64_t nt = (n + 31) / 32;
-  return (size_t)nt * img_tile_bytes(d, kind) + (size_t)nt * 128;
+  return (size_t)nt * img_tile_bytes(d, kind) + (size_t)nt * 128 +
+         (kind == IMG_SORTED ? (size_t)nt * 256 : 0);
 }
 
 XImage x_image_view(const void *image, int64_t n, int64_t d, int kind) {
+  const int64_t nt = (n + 31) / 32;
   XImage im;
   im.tiles = (const uint16_t *)image;
   im.xx = (const float *)((const char *)image +
-                          (size_t)((n + 31) / 32) * img_tile_bytes(d, kind));
+                          (size_t)nt * img_tile_bytes(d, kind));
   im.kind = kind;
+  im.perm = nullptr;
+  im.plab = nullptr;
+  if (kind == IMG_SORTED) {
+    im.perm = (const int32_t *)(im.xx + nt * 32);
+    im.plab = (int32_t *)(im.perm + nt * 32);
+  }
   return im;
 }
 
@@ -1052,21 +975,30 @@ XImage x_image_view(const void *image, int64_t n, int64_t d, int kind) {
 // with consecutive lanes on consecutive features (whole lines), staged as
 // fp32 in LDS, then written in operand order with the same fp64 -> fp32 ->
 // bf16 roundings the converting screens apply.  |x|^2 is summed in fp64
-// over the fp32 values and rounded once.
+// over the fp32 values and rounded once.  perm != nullptr (IMG_SORTED):
+// image row i holds sample perm[i] (-1: a zero row past the data).
 template <class TX, int NKS>
 __global__ void __launch_bounds__(256)
     k_x_image(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
-              uint16_t *__restrict__ tiles, float *__restrict__ xx) {
+              const int32_t *__restrict__ perm, uint16_t *__restrict__ tiles,
+              float *__restrict__ xx) {
   constexpr int DP = 16 * NKS, LD = DP + 4;
   __shared__ float s[32 * LD];
+  __shared__ int64_t srow[32];
   const int64_t nt = (n + 31) / 32;
   for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
     const int64_t r0 = t * 32;
     __syncthreads();  // the previous tile's reads are done
+    if (threadIdx.x < 32) {
+      const int64_t i = r0 + threadIdx.x;
+      srow[threadIdx.x] = perm ? (int64_t)perm[i] : (i < n ? i : -1);
+    }
+    __syncthreads();
     for (int e = threadIdx.x; e < 32 * DP; e += 256) {
       const int row = e / DP, col = e % DP;
+      const int64_t src = srow[row];
       float v = 0.f;
-      if (r0 + row < n && col < d) v = (float)X[(r0 + row) * ldx + col];
+      if (src >= 0 && col < d) v = (float)X[src * ldx + col];
       s[row * LD + col] = v;
     }
     __syncthreads();
@@ -1143,24 +1075,18 @@ __global__ void __launch_bounds__(256)
 }
 
 template <class TX>
-int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, int kind,
-                   void *image, int cus, hipStream_t s) {
-  const XImage im = x_image_view(image, n, d, kind);
+static int launch_image_tiles(const TX *X, int64_t n, int d, int64_t ldx,
+                              const int32_t *perm, const XImage &im, int cus,
+                              hipStream_t s) {
   const int64_t nt = (n + 31) / 32;
   const unsigned g =
       (unsigned)std::max<int64_t>(1, std::min<int64_t>(nt, (int64_t)cus * 8));
-  uint16_t *tiles = (uint16_t *)image;
+  uint16_t *tiles = (uint16_t *)im.tiles;
   float *xx = (float *)im.xx;
-  if (kind == IMG_SPLIT) {
-    if (d > 32) return fail(DKM_E_ARG, "x_image: split image needs d <= 32");
-    k_x_image_split<TX><<<g, 256, 0, s>>>(X, n, d, ldx, tiles, xx);
-    return check_launch("sample image (split)");
-  }
-  if (kind != IMG_SINGLE) return fail(DKM_E_ARG, "x_image: bad kind");
   switch ((int)(dpad16(d) / 16)) {
 #define DKM_XI(N)                                                         \
   case N:                                                                 \
-    k_x_image<TX, N><<<g, 256, 0, s>>>(X, n, d, ldx, tiles, xx);          \
+    k_x_image<TX, N><<<g, 256, 0, s>>>(X, n, d, ldx, perm, tiles, xx);    \
     break;
     DKM_XI(1) DKM_XI(2) DKM_XI(3) DKM_XI(4)
     DKM_XI(5) DKM_XI(6) DKM_XI(7) DKM_XI(8)
@@ -1171,36 +1097,141 @@ int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, int kind,
   return check_launch("sample image");
 }
 
+template <class TX>
+int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, int kind,
+                   void *image, int cus, hipStream_t s) {
+  const XImage im = x_image_view(image, n, d, kind);
+  if (kind == IMG_SPLIT) {
+    if (d > 32) return fail(DKM_E_ARG, "x_image: split image needs d <= 32");
+    const int64_t nt = (n + 31) / 32;
+    const unsigned g = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>(nt, (int64_t)cus * 8));
+    k_x_image_split<TX><<<g, 256, 0, s>>>(X, n, d, ldx, (uint16_t *)image,
+                                          (float *)im.xx);
+    return check_launch("sample image (split)");
+  }
+  if (kind != IMG_SINGLE) return fail(DKM_E_ARG, "x_image: bad kind");
+  return launch_image_tiles<TX>(X, n, d, ldx, nullptr, im, cus, s);
+}
+
 template int launch_x_image<double>(const double *, int64_t, int, int64_t,
                                     int, void *, int, hipStream_t);
 template int launch_x_image<float>(const float *, int64_t, int, int64_t, int,
                                    void *, int, hipStream_t);
 
+// ---- IMG_SORTED: the image with its rows grouped by label ----------------
+// perm[i] for i in [0, ntot): the sorted indices (labels in [0, k)), then
+// the samples whose label is outside [0, k) (appended by
+// k_perm_unlabelled), then -1 for the padding rows past n.
+__global__ void k_perm_sorted(const int32_t *__restrict__ sitems,
+                              const int32_t *__restrict__ nsorted, int64_t n,
+                              int64_t ntot, int32_t *__restrict__ perm) {
+  const int64_t m = *nsorted;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ntot;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < m) perm[i] = sitems[i];
+    else if (i >= n) perm[i] = -1;
+  }
+}
+
+__global__ void k_perm_unlabelled(const int32_t *__restrict__ lab, int64_t n,
+                                  int k, const int32_t *__restrict__ nsorted,
+                                  unsigned long long *count,
+                                  int32_t *__restrict__ perm) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = *nsorted;
+  for (int64_t i0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63ll;
+       i0 < n; i0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = i0 + lane;
+    const bool un = i < n && (unsigned)lab[i] >= (unsigned)k;
+    const uint64_t b = __ballot(un);
+    if (!b) continue;
+    unsigned long long at = 0;
+    if (lane == 0) at = atomicAdd(count, (unsigned long long)__popcll(b));
+    at = __shfl(at, 0, 64);
+    if (un) perm[m + (int64_t)at + lane_prefix(b)] = (int32_t)i;
+  }
+}
+
+// plab[i] = lab[perm[i]] (init), or only where plab[i] < 0 (sync: the rows
+// whose label a re-check kernel wrote after the screen)
+__global__ void k_plab(const int32_t *__restrict__ perm,
+                       const int32_t *__restrict__ lab, int64_t ntot,
+                       int32_t *__restrict__ plab, int only_marked) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ntot;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (only_marked && plab[i] >= 0) continue;
+    const int32_t p = perm[i];
+    plab[i] = p >= 0 ? lab[p] : -1;
+  }
+}
+
+static unsigned flat_grid(int64_t n, int cus) {
+  return (unsigned)std::max<int64_t>(
+      1, std::min<int64_t>((n + 255) / 256, (int64_t)cus * 16));
+}
+
+template <class TX>
+int launch_x_image_sorted(const TX *X, int64_t n, int d, int64_t ldx,
+                          const int32_t *labels, int k, const WsView &v,
+                          void *image, int cus, hipStream_t s) {
+  const XImage im = x_image_view(image, n, d, IMG_SORTED);
+  const int64_t ntot = (n + 31) / 32 * 32;
+  int32_t *perm = (int32_t *)im.perm;
+  if (int r = sort_by_label(labels, 0, n, k, v, s)) return r;
+  unsigned long long *cnt = (unsigned long long *)&v.hdr->reserved[3];
+  if (hipMemsetAsync(cnt, 0, 8, s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "sorted image: memset");
+  const unsigned g = flat_grid(ntot, cus);
+  k_perm_sorted<<<g, 256, 0, s>>>(v.sitems, v.soff + k, n, ntot, perm);
+  k_perm_unlabelled<<<g, 256, 0, s>>>(labels, n, k, v.soff + k, cnt, perm);
+  k_plab<<<g, 256, 0, s>>>(perm, labels, ntot, im.plab, 0);
+  if (int r = check_launch("sorted image: permutation")) return r;
+  return launch_image_tiles<TX>(X, n, d, ldx, perm, im, cus, s);
+}
+
+template int launch_x_image_sorted<double>(const double *, int64_t, int,
+                                           int64_t, const int32_t *, int,
+                                           const WsView &, void *, int,
+                                           hipStream_t);
+template int launch_x_image_sorted<float>(const float *, int64_t, int,
+                                          int64_t, const int32_t *, int,
+                                          const WsView &, void *, int,
+                                          hipStream_t);
+
+int launch_plab_sync(const XImage &img, int64_t n, const int32_t *lab,
+                     int cus, hipStream_t s) {
+  if (img.kind != IMG_SORTED) return 0;
+  const int64_t ntot = (n + 31) / 32 * 32;
+  k_plab<<<flat_grid(ntot, cus), 256, 0, s>>>(img.perm, lab, ntot, img.plab,
+                                              1);
+  return check_launch("sorted image: label sync");
+}
+
 template <class TX>
 int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
                      const WsView &v, int32_t *lab_out, int64_t base, int hint,
-                     int cus, hipStream_t s, int *nseg, XImage img,
-                     float4 *bnd) {
-  const bool pc = b2pc_enabled() && SB2 / 64 > B2_NLOAD &&
-                  b2pc_lds_bytes(k, d) <= 160 * 1024;
-  const size_t lds = pc ? b2pc_lds_bytes(k, d) : b2_lds_bytes(k, d);
+                     int cus, hipStream_t s, int *nseg, XImage img) {
+  const size_t lds = b2_lds_bytes(k, d);
   if (lds > 160 * 1024) return 1;  // caller uses k_screen_b1
-  // the image path reads whole tiles: the range must start on one
-  const bool im = img.tiles && img.kind == IMG_SINGLE && !pc && base % 32 == 0;
-  if (!im) img = XImage{nullptr, nullptr, IMG_NONE};
+  // the image paths read whole tiles: the range must start on one (the
+  // sorted image covers the whole range: its rows are not sample rows)
+  int ik = img.tiles ? img.kind : IMG_NONE;
+  if (ik == IMG_SORTED && base != 0)
+    return fail(DKM_E_ARG, "screen_b2: the sorted image needs the whole range");
+  if (ik == IMG_SINGLE && base % 32 != 0) ik = IMG_NONE;
+  if (ik != IMG_SINGLE && ik != IMG_SORTED) ik = IMG_NONE;
   const int nks = (int)(dpad16(d) / 16);
   const bool w1 = kpad32(k) <= 1024;
   const void *kf = nullptr;
-#define DKM_B2K(N, W, P, I) (const void *)k_screen_b2<TX, N, W, P, I>
+#define DKM_B2K(N, W, I) (const void *)k_screen_b2<TX, N, W, I>
+#define DKM_B2W(N, I) (w1 ? DKM_B2K(N, true, I) : DKM_B2K(N, false, I))
   switch (nks) {
 #define DKM_B2(N)                                                          \
   case N:                                                                  \
-    kf = pc ? (w1 ? DKM_B2K(N, true, true, false)                          \
-                  : DKM_B2K(N, false, true, false))                        \
-       : im ? (w1 ? DKM_B2K(N, true, false, true)                          \
-                  : DKM_B2K(N, false, false, true))                        \
-            : (w1 ? DKM_B2K(N, true, false, false)                         \
-                  : DKM_B2K(N, false, false, false));                      \
+    kf = ik == IMG_SORTED   ? DKM_B2W(N, IMG_SORTED)                       \
+         : ik == IMG_SINGLE ? DKM_B2W(N, IMG_SINGLE)                       \
+                            : DKM_B2W(N, IMG_NONE);                        \
     break;
     DKM_B2(1) DKM_B2(2) DKM_B2(3) DKM_B2(4)
     DKM_B2(5) DKM_B2(6) DKM_B2(7) DKM_B2(8)
@@ -1208,16 +1239,16 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
     default:
       return fail(DKM_E_ARG, "screen_b2: d too large");
   }
+#undef DKM_B2W
+#undef DKM_B2K
   if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return fail(DKM_E_LAUNCH, "screen_b2: LDS attribute");
-  const int nw = pc ? SB2 / 64 - B2_NLOAD : SB2 / 64;  // screening waves
-  const int64_t need = pc ? (end - base + 31) / 32
-                          : (end - base + 32 * nw - 1) / (32 * nw);
+  const int nw = SB2 / 64;  // screening waves
+  const int64_t need = (end - base + 32 * nw - 1) / (32 * nw);
   const unsigned g =
       (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)cus));
   *nseg = (int)std::min<int64_t>((int64_t)g * nw, std::min(TL_SEGS, B1_SEGS));
-  const int delta = 0;  // labels only (the sums come from the labels)
   B2View bv;
   bv.hdr = v.hdr;
   bv.b1frag = v.b1frag;
@@ -1229,22 +1260,19 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
   bv.tcount = v.tcount;
   bv.ccount = v.ccount;
   bv.ncount = v.ncount;
-  bv.bnd = bnd;
+  bv.mind = ik == IMG_SORTED ? v.mind : nullptr;
   hipLaunchKernelGGL((void (*)(const TX *, int64_t, int, int64_t, int, B2View,
-                               int32_t *, int64_t, int, int, XImage))kf,
+                               int32_t *, int64_t, int, XImage))kf,
                      dim3(g), dim3(SB2), lds, s, X, end, d, ldx, k, bv,
-                     lab_out, base, delta, hint, img);
-#undef DKM_B2K
+                     lab_out, base, hint, img);
   return check_launch("screen assignment (single product, centres on lanes)");
 }
 
 template int launch_screen_b2<double>(const double *, int64_t, int, int64_t,
                                       int, const WsView &, int32_t *, int64_t,
-                                      int, int, hipStream_t, int *, XImage,
-                                      float4 *);
+                                      int, int, hipStream_t, int *, XImage);
 template int launch_screen_b2<float>(const float *, int64_t, int, int64_t, int,
                                      const WsView &, int32_t *, int64_t, int,
-                                     int, hipStream_t, int *, XImage,
-                                     float4 *);
+                                     int, hipStream_t, int *, XImage);
 
 }  // namespace dkm

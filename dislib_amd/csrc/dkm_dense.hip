@@ -2770,7 +2770,7 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                          int64_t ldx, const double *C, int k, const WsView &v,
                          size_t wsb, int32_t *labels, double *acc,
                          int acc_kind, hipStream_t s, XImage img,
-                         float4 *bnd = nullptr) {
+                         bool nohint = false, bool force_b1 = false) {
   (void)wsb;
   const int64_t nq = std::min<int64_t>(v.nq, INT32_MAX);
   if (!labels && nq < 1)
@@ -2783,9 +2783,10 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const bool b1 = prec == P_B1 && v.b1frag && vec &&
                   (int64_t)32 * ldx * (int64_t)sizeof(TX) < (1ll << 31) &&
                   (acc_kind == 0 || acc_kind == 1 || (labels && nq >= n));
-  if (bnd && !b1)
-    return fail(DKM_E_ARG, "screen: bounds need the single-product screen");
   if (prec == P_B1 && !b1) prec = P_B3;
+  if (img.kind == IMG_SORTED && !b1)
+    return fail(DKM_E_ARG, "screen: the sorted image needs the single-product "
+                           "screen (16-B aligned rows)");
   // d <= 32 bf16x3 with the 32x32x16 fragments resident: k_screen_w32
   const size_t fb32 = (size_t)(kpad32(k) / 32) * (4096 + 128);
   const bool w32 = prec == P_B3 && d <= 32 && vec && fb32 <= LDS_BUDGET &&
@@ -2823,13 +2824,14 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
     int r, nseg = 0;
     if (b1) {
       // the incoming labels (previous iteration) seed the threshold pass
-      const int hint = labels && acc_kind != 0 ? 1 : 0;
-      r = b2_enabled() ? launch_screen_b2<TX>(X, end, d, ldx, k, v, lab_out,
-                                              base, hint, dev_info().cus, s,
-                                              &nseg, img, bnd)
-                       : 1;
-      if (r == 1 && bnd)
-        return fail(DKM_E_ARG, "screen: bounds need k_screen_b2");
+      // (NOHINT: the caller knows them to be poor, e.g. labels of the
+      // initial centres -- the top-3 pass runs directly)
+      const int hint = labels && acc_kind != 0 && !nohint ? 1 : 0;
+      r = force_b1 ? 1
+                   : launch_screen_b2<TX>(X, end, d, ldx, k, v, lab_out, base,
+                                          hint, dev_info().cus, s, &nseg, img);
+      if (r == 1 && img.kind == IMG_SORTED)
+        return fail(DKM_E_ARG, "screen: the sorted image needs k_screen_b2");
       if (r == 1)
         r = launch_screen_b1<TX>(X, end, d, ldx, k, v, lab_out, base, hint, s,
                                  &nseg);
@@ -2861,6 +2863,9 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
       return r;
     if ((r = launch_recheck<TX>(X, end, d, ldx, k, v, lab_out, acc,
                                 skind, vec, base, s)))
+      return r;
+    // the sorted image's label copy: the rows the re-checks decided
+    if (b1 && (r = launch_plab_sync(img, n, labels, dev_info().cus, s)))
       return r;
     if (post && (r = launch_post_sums<TX>(X, base, end, d, ldx, lab_out,
                                           prevbuf, k, acc, v, s)))
@@ -2922,6 +2927,10 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
   if (!labels && !acc)
     return fail(DKM_E_ARG, std::string(who) + ": nothing to write");
   hipStream_t s = (hipStream_t)stream;
+  if (mode & ~(DKM_MODE_MASK | DKM_MODE_NOHINT | DKM_MODE_B1))
+    return fail(DKM_E_ARG, std::string(who) + ": unknown mode flags");
+  const bool nohint = mode & DKM_MODE_NOHINT, force_b1 = mode & DKM_MODE_B1;
+  mode &= DKM_MODE_MASK;
   if (mode == DKM_MODE_AUTO)
     mode = !screen_ok(k, d) && !gemm_path(k, d) ? DKM_MODE_EXACT
            // the GEMM screen (d > 128) and sums beyond LDS with the bf16
@@ -2930,6 +2939,13 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                    (screen_ok(k, d) && b1_ok(k, d) && !sums_fit_lds(k, d))
                ? DKM_MODE_SCREEN_BF16
                : DKM_MODE_SCREEN_BF16X3;
+  // the sorted image keeps a copy of the labels that only k_screen_b2
+  // maintains: any other arithmetic would leave it stale
+  if (image && image_kind == IMG_SORTED &&
+      (mode != DKM_MODE_SCREEN_BF16 || !screen_ok(k, d) || !labels || force_b1))
+    return fail(DKM_E_ARG, std::string(who) +
+                               ": the sorted image needs the single-product "
+                               "screen (MODE_SCREEN_BF16 or AUTO) and labels");
   if (mode == DKM_MODE_EXACT)
     return launch_exact<TX>(X, n, (int)d, ldx, C, (int)k, labels, acc,
                             acc_kind, s);
@@ -2951,9 +2967,10 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                      : mode == DKM_MODE_SCREEN_BF16 ? P_B1
                                                     : P_B3;
     const XImage img = image ? x_image_view(image, n, d, image_kind)
-                             : XImage{nullptr, nullptr, IMG_NONE};
+                             : XImage{nullptr, nullptr, IMG_NONE, nullptr,
+                                      nullptr};
     return launch_screen<TX>(prec, X, n, (int)d, ldx, C, (int)k, v, wsb,
-                             labels, acc, acc_kind, s, img);
+                             labels, acc, acc_kind, s, img, nohint, force_b1);
   }
   return fail(DKM_E_ARG, std::string(who) + ": bad mode");
 }
@@ -2975,83 +2992,27 @@ static int x_image(const TX *X, int64_t n, int64_t d, int64_t ldx, int kind,
                             (hipStream_t)stream);
 }
 
-// ---- dkm_assign_pruned_*: bound-based skipping (dkm_prune.hip) ----------
-static bool prune_ok(int64_t k, int64_t d) {
-  return d <= 128 && d % 8 == 0 && k >= 2 && k <= INT32_MAX &&
-         !gemm_path(k, d) && screen_ok(k, d) && b1_ok(k, d) && b2_enabled() &&
-         b2_lds_bytes(k, d) <= 160 * 1024;
-}
-
 template <class TX>
-static int assign_pruned(const TX *X, const void *image, int image_kind,
-                         int64_t n, int64_t d,
-                         int64_t ldx, const double *C, const double *Cp,
-                         int64_t k, const void *ws, size_t wsb,
-                         int32_t *labels, double *delta, void *state,
-                         size_t sb, int init, int64_t *n_active, void *stream,
-                         const char *who) {
+static int x_image_sorted(const TX *X, int64_t n, int64_t d, int64_t ldx,
+                          const int32_t *labels, int64_t k, const void *ws,
+                          size_t wsb, void *image, size_t image_bytes,
+                          void *stream, const char *who) {
   const std::string w(who);
-  if (n < 0 || d <= 0 || k <= 0 || ldx < d) return fail(DKM_E_ARG, w + ": bad n/d/k/ldx");
-  if (!labels || !delta || !state || !C || (!init && !Cp))
-    return fail(DKM_E_ARG, w + ": NULL argument");
-  if (!prune_ok(k, d))
-    return fail(DKM_E_ARG, w + ": needs the single-product screen "
-                               "(d <= 128, d % 8 == 0, k x d within LDS)");
-  if (((uintptr_t)X % 16) != 0 || ldx % (16 / (int64_t)sizeof(TX)) != 0 ||
-      (int64_t)32 * ldx * (int64_t)sizeof(TX) >= (1ll << 31))
-    return fail(DKM_E_ARG, w + ": X rows must be 16-B aligned");
-  if (sb < prune_state_bytes(n, k, d))
-    return fail(DKM_E_WORKSPACE, w + ": state buffer too small");
-  if (n_active) *n_active = 0;
+  if (n < 0 || d <= 0 || ldx < d || k <= 1 || k > INT32_MAX)
+    return fail(DKM_E_ARG, w + ": bad n/d/k/ldx");
+  if (n > INT32_MAX) return fail(DKM_E_ARG, w + ": n > 2^31 - 1");
   if (n == 0) return 0;
-  hipStream_t s = (hipStream_t)stream;
+  if (!X || !labels || !image) return fail(DKM_E_ARG, w + ": NULL");
+  if (!dkm_x_image_sorted_ok(k, d))
+    return fail(DKM_E_ARG, w + ": (k, d) does not take the sorted image");
+  if (image_bytes < x_image_bytes(n, d, IMG_SORTED))
+    return fail(DKM_E_WORKSPACE, w + ": image too small");
   WsView v;
   if (int r = ws_view(ws, wsb, k, d, &v)) return r;
-  const PruneView p = prune_view(state, n, k, d);
-  int64_t na = n;
-  if (!init) {
-    if (int r = launch_prune<TX>(X, ldx, C, Cp, k, d, labels, p, s)) return r;
-    if (hipMemcpyAsync(&na, p.bcnt + p.nb, 8, hipMemcpyDeviceToHost, s) !=
-            hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return fail(DKM_E_LAUNCH, w + ": active count");
-  }
-  if (n_active) *n_active = na;
-  const int64_t cap = std::min<int64_t>(p.cap, v.nq) / 32 * 32;
-  if (cap < 32) return fail(DKM_E_WORKSPACE, w + ": label scratch too small");
-  // most samples active: screen X in place (through the image when given)
-  const bool gather = !init && na * 5 <= n * 2;
-  const int64_t total = gather ? na : n;
-  const int nks = (int)(dpad16(d) / 16);
-  const XImage img0 = image && image_kind == IMG_SINGLE
-                         ? x_image_view(image, n, d, IMG_SINGLE)
-                         : XImage{nullptr, nullptr, IMG_NONE};
-  for (int64_t j0 = 0; j0 < total; j0 += cap) {
-    const int64_t m = std::min(cap, total - j0);
-    const TX *Xc;
-    int64_t ldc;
-    int32_t *lc;
-    XImage img{nullptr, nullptr, IMG_NONE};
-    if (gather) {
-      if (int r = launch_prune_gather<TX>(X, ldx, (int)d, p, j0, m, labels, s))
-        return r;
-      Xc = (const TX *)p.xa;
-      ldc = d;
-      lc = p.la;
-    } else {
-      Xc = X + j0 * ldx;
-      ldc = ldx;
-      lc = labels + j0;
-      if (img0.tiles)
-        img = XImage{img0.tiles + (j0 / 32) * nks * 512, img0.xx + j0,
-                     IMG_SINGLE};
-    }
-    if (int r = launch_screen<TX>(P_B1, Xc, m, (int)d, ldc, C, (int)k, v, wsb,
-                                  lc, delta, 2, s, img, p.bnd))
-      return r;
-    if (int r = launch_prune_final(gather, p, j0, m, lc, labels, s)) return r;
-  }
-  return 0;
+  if (!sorted_sums_ok(k, n, v))
+    return fail(DKM_E_WORKSPACE, w + ": workspace label scratch < n");
+  return launch_x_image_sorted<TX>(X, n, (int)d, ldx, labels, (int)k, v, image,
+                                   dev_info().cus, (hipStream_t)stream);
 }
 
 template <class TX>
@@ -3131,11 +3092,12 @@ int dkm_predict_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
 int dkm_x_image_kind(int64_t k, int64_t d, int mode) {
   if (k <= 0 || d <= 0 || d > 128 || k > INT32_MAX) return IMG_NONE;
   if (gemm_path(k, d) || !screen_ok(k, d)) return IMG_NONE;
+  mode &= DKM_MODE_MASK;
   if (mode == DKM_MODE_AUTO)
     mode = b1_ok(k, d) && !sums_fit_lds(k, d) ? DKM_MODE_SCREEN_BF16
                                               : DKM_MODE_SCREEN_BF16X3;
   if (mode == DKM_MODE_SCREEN_BF16)
-    return b1_ok(k, d) && b2_enabled() && b2_lds_bytes(k, d) <= 160 * 1024
+    return b1_ok(k, d) && b2_lds_bytes(k, d) <= 160 * 1024
                ? IMG_SINGLE
                : IMG_NONE;
   if (mode == DKM_MODE_SCREEN_BF16X3)
@@ -3149,7 +3111,7 @@ int dkm_x_image_kind(int64_t k, int64_t d, int mode) {
 size_t dkm_x_image_bytes(int64_t n, int64_t d, int kind) {
   if (n < 0 || d <= 0 || d > 128) return 0;
   if (kind == IMG_SPLIT && d > 32) return 0;
-  if (kind != IMG_SINGLE && kind != IMG_SPLIT) return 0;
+  if (kind != IMG_SINGLE && kind != IMG_SPLIT && kind != IMG_SORTED) return 0;
   return x_image_bytes(n, d, kind);
 }
 
@@ -3165,88 +3127,86 @@ int dkm_x_image_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
                         "dkm_x_image_f32");
 }
 
+int dkm_x_image_sorted_ok(int64_t k, int64_t d) {
+  return k > 1 && k <= INT32_MAX && d > 0 && d <= 128 &&
+                 dkm_x_image_kind(k, d, DKM_MODE_SCREEN_BF16) == IMG_SINGLE &&
+                 mind_ok(k, d)
+             ? 1
+             : 0;
+}
+
+int dkm_x_image_sorted_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
+                           const int32_t *labels, int64_t k, const void *ws,
+                           size_t ws_bytes, void *image, size_t image_bytes,
+                           void *stream) {
+  return x_image_sorted<double>(X, n, d, ldx, labels, k, ws, ws_bytes, image,
+                                image_bytes, stream, "dkm_x_image_sorted_f64");
+}
+
+int dkm_x_image_sorted_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
+                           const int32_t *labels, int64_t k, const void *ws,
+                           size_t ws_bytes, void *image, size_t image_bytes,
+                           void *stream) {
+  return x_image_sorted<float>(X, n, d, ldx, labels, k, ws, ws_bytes, image,
+                               image_bytes, stream, "dkm_x_image_sorted_f32");
+}
+
+#define DKM_IMG_CHECK(who)                                                  \
+  if (image && image_bytes < dkm_x_image_bytes(n, d, image_kind))           \
+    return fail(DKM_E_ARG, std::string(who) +                               \
+                               ": image_bytes does not match n, d and kind");
+
 int dkm_partial_sum_img_f64(const double *X, const void *image, int image_kind,
-                             int64_t n,
-                            int64_t d, int64_t ldx, const double *C,
-                            int64_t k, const void *ws, size_t ws_bytes,
-                            int32_t *labels, double *acc, int mode,
-                            void *stream) {
+                            size_t image_bytes, int64_t n, int64_t d,
+                            int64_t ldx, const double *C, int64_t k,
+                            const void *ws, size_t ws_bytes, int32_t *labels,
+                            double *acc, int mode, void *stream) {
   if (!acc) return fail(DKM_E_ARG, "partial_sum: acc is NULL");
+  DKM_IMG_CHECK("dkm_partial_sum_img_f64")
   return assign<double>(X, n, d, ldx, C, k, ws, ws_bytes, labels, acc, 1,
                         mode, stream, "dkm_partial_sum_img_f64", image,
                         image_kind);
 }
 
 int dkm_partial_sum_img_f32(const float *X, const void *image, int image_kind,
-                             int64_t n,
-                            int64_t d, int64_t ldx, const double *C,
-                            int64_t k, const void *ws, size_t ws_bytes,
-                            int32_t *labels, double *acc, int mode,
-                            void *stream) {
+                            size_t image_bytes, int64_t n, int64_t d,
+                            int64_t ldx, const double *C, int64_t k,
+                            const void *ws, size_t ws_bytes, int32_t *labels,
+                            double *acc, int mode, void *stream) {
   if (!acc) return fail(DKM_E_ARG, "partial_sum: acc is NULL");
+  DKM_IMG_CHECK("dkm_partial_sum_img_f32")
   return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, acc, 1,
                        mode, stream, "dkm_partial_sum_img_f32", image,
-                        image_kind);
+                       image_kind);
 }
 
-int dkm_assign_delta_img_f64(const double *X, const void *image, int image_kind,
-                              int64_t n,
+int dkm_assign_delta_img_f64(const double *X, const void *image,
+                             int image_kind, size_t image_bytes, int64_t n,
                              int64_t d, int64_t ldx, const double *C,
                              int64_t k, const void *ws, size_t ws_bytes,
                              int32_t *labels, double *delta, int mode,
                              void *stream) {
   if (!labels || !delta)
     return fail(DKM_E_ARG, "assign_delta: labels and delta are required");
+  DKM_IMG_CHECK("dkm_assign_delta_img_f64")
   return assign<double>(X, n, d, ldx, C, k, ws, ws_bytes, labels, delta, 2,
                         mode, stream, "dkm_assign_delta_img_f64", image,
                         image_kind);
 }
 
 int dkm_assign_delta_img_f32(const float *X, const void *image, int image_kind,
-                              int64_t n,
-                             int64_t d, int64_t ldx, const double *C,
-                             int64_t k, const void *ws, size_t ws_bytes,
-                             int32_t *labels, double *delta, int mode,
-                             void *stream) {
+                             size_t image_bytes, int64_t n, int64_t d,
+                             int64_t ldx, const double *C, int64_t k,
+                             const void *ws, size_t ws_bytes, int32_t *labels,
+                             double *delta, int mode, void *stream) {
   if (!labels || !delta)
     return fail(DKM_E_ARG, "assign_delta: labels and delta are required");
+  DKM_IMG_CHECK("dkm_assign_delta_img_f32")
   return assign<float>(X, n, d, ldx, C, k, ws, ws_bytes, labels, delta, 2,
                        mode, stream, "dkm_assign_delta_img_f32", image,
-                        image_kind);
+                       image_kind);
 }
-
-size_t dkm_prune_state_bytes(int64_t n, int64_t k, int64_t d) {
-  if (n < 0 || k <= 0 || d <= 0) return 0;
-  return prune_state_bytes(n, k, d);
-}
-
-int dkm_prune_supported(int64_t k, int64_t d) { return prune_ok(k, d) ? 1 : 0; }
-
-int dkm_assign_pruned_f64(const double *X, const void *image, int image_kind,
-                           int64_t n,
-                          int64_t d, int64_t ldx, const double *C,
-                          const double *C_prev, int64_t k, const void *ws,
-                          size_t ws_bytes, int32_t *labels, double *delta,
-                          void *state, size_t state_bytes, int init,
-                          int64_t *n_active, void *stream) {
-  return assign_pruned<double>(X, image, image_kind, n, d, ldx, C, C_prev, k,
-                               ws, ws_bytes,
-                               labels, delta, state, state_bytes, init,
-                               n_active, stream, "dkm_assign_pruned_f64");
-}
-
-int dkm_assign_pruned_f32(const float *X, const void *image, int image_kind,
-                           int64_t n,
-                          int64_t d, int64_t ldx, const double *C,
-                          const double *C_prev, int64_t k, const void *ws,
-                          size_t ws_bytes, int32_t *labels, double *delta,
-                          void *state, size_t state_bytes, int init,
-                          int64_t *n_active, void *stream) {
-  return assign_pruned<float>(X, image, image_kind, n, d, ldx, C, C_prev, k,
-                              ws, ws_bytes,
-                              labels, delta, state, state_bytes, init,
-                              n_active, stream, "dkm_assign_pruned_f32");
-}
+#undef DKM_IMG_CHECK
 
 int dkm_label_sums_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
                        const int32_t *labels, int64_t k, const void *ws,

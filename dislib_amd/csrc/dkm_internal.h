@@ -119,6 +119,10 @@ struct WsView {
   int32_t *ncount; // b1_ok: entries used per screen wave
   int2 *tlist;    // TL_SEGS x TL_CAP undecided (offset, prev) per screen wave
   int32_t *tcount; // TL_SEGS entries used per screen wave
+  // block skipping of k_screen_b2 (mind_ok(k, d), else NULL): k x MIND_LD
+  // lower bounds of the distance from centre p to the nearest other centre
+  // of each 32-centre block (+inf past the last block)
+  float *mind;
   // GEMM screen (gemm_path only; else NULL)
   char *gfrag;     // kpad256 x dpad32 centre tiles (-2c, bf16 hi/lo)
   char *gfrag1;    // kpad256 x dpad64 centre tiles (-2c, bf16 hi only:
@@ -144,9 +148,13 @@ struct WsView {
 // Single-product screen with the centres on the lanes (dkm_b2.hip): the
 // threshold pass without per-block norm reads.  Returns 1 (nothing
 // launched) when its LDS image does not fit; the caller runs k_screen_b1.
-bool b2_enabled();
 int b2_probe();  // != 0: a result-invalidating timing probe build
 size_t b2_lds_bytes(int64_t k, int64_t d);
+// the block-skip table (WsView::mind): 32-centre blocks per row
+constexpr int MIND_LD = 64;
+inline bool mind_ok(int64_t k, int64_t d) {
+  return b1_ok(k, d) && (k + 31) / 32 <= MIND_LD;
+}
 // The sample image (dkm_x_image_*): a resident bf16 copy of X in the
 // operand order of the screen that reads it, then fp32 |x|^2 per row
 // (rows and features past n, d zero).  Kinds:
@@ -155,11 +163,18 @@ size_t b2_lds_bytes(int64_t k, int64_t d);
 //  IMG_SPLIT (k_screen_w32, d <= 32): 32-row tiles of 4 x 1 KB (hi K-slice
 //    0, hi 1, lo 0, lo 1), lane l of slice s = row l & 31, features
 //    16 (l >> 5) + 8 s .. + 7, hi = bf16(fl32(x)), lo = bf16(fl32(x) - hi).
-constexpr int IMG_NONE = 0, IMG_SINGLE = 1, IMG_SPLIT = 2;
+//  IMG_SORTED (k_screen_b2 with block skipping): the IMG_SINGLE layout over
+//    the rows perm[0 .. nt*32) -- the samples grouped by a label vector --
+//    then int32 perm (sample of each image row, -1 past n) and int32 plab
+//    (the current label of each image row: the screen's hints, kept equal
+//    to labels[perm[i]] by the screen and k_plab sync).
+constexpr int IMG_NONE = 0, IMG_SINGLE = 1, IMG_SPLIT = 2, IMG_SORTED = 3;
 struct XImage {
   const uint16_t *tiles;
   const float *xx;
   int kind;
+  const int32_t *perm;  // IMG_SORTED only
+  int32_t *plab;        // IMG_SORTED only
 };
 size_t x_image_bytes(int64_t n, int64_t d, int kind);
 XImage x_image_view(const void *image, int64_t n, int64_t d, int kind);
@@ -167,38 +182,18 @@ template <class TX>
 int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, int kind,
                    void *image, int cus, hipStream_t s);
 template <class TX>
+int launch_x_image_sorted(const TX *X, int64_t n, int d, int64_t ldx,
+                          const int32_t *labels, int k, const WsView &v,
+                          void *image, int cus, hipStream_t s);
+// IMG_SORTED: plab <- labels[perm] where the screen marked it (-1) for a
+// re-check kernel; no-op for the other kinds
+int launch_plab_sync(const XImage &img, int64_t n, const int32_t *lab,
+                     int cus, hipStream_t s);
+template <class TX>
 int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
                      const WsView &v, int32_t *lab_out, int64_t base,
                      int hint, int cus, hipStream_t s, int *nseg,
-                     XImage img, float4 *bnd = nullptr);
-
-// Bound-based skipping of samples whose label cannot change
-// (dkm_prune.hip; the state buffer of dkm_assign_pruned_*).
-struct PruneView {
-  int64_t n, nb, cap;
-  float2 *ul;      // n (upper, lower) distance bounds
-  int32_t *act;    // n active sample indices
-  uint64_t *mask;  // ceil(n / 64) active bits
-  int64_t *bcnt;   // nb + 1 range counts / offsets (bcnt[nb] = total)
-  float *drift;    // kpad32 centre moves
-  float *dstat;    // max move, second max, argmax (int bits)
-  char *xa;        // cap gathered rows (TX, ld = d)
-  int32_t *la;     // cap gathered labels
-  float4 *bnd;     // cap bounds from k_screen_b2
-};
-size_t prune_state_bytes(int64_t n, int64_t k, int64_t d);
-PruneView prune_view(void *state, int64_t n, int64_t k, int64_t d);
-template <class TX>
-int launch_prune(const TX *X, int64_t ldx, const double *C, const double *Cp,
-                 int64_t k, int64_t d, const int32_t *lab, const PruneView &p,
-                 hipStream_t s);
-template <class TX>
-int launch_prune_gather(const TX *X, int64_t ldx, int d, const PruneView &p,
-                        int64_t j0, int64_t m, const int32_t *lab,
-                        hipStream_t s);
-int launch_prune_final(bool gathered, const PruneView &p, int64_t j0,
-                       int64_t m, const int32_t *la, int32_t *lab,
-                       hipStream_t s);
+                     XImage img);
 
 // Sorted sums: counting sort of the sample indices by label (LDS histograms
 // of k bins: k <= SORT_KMAX), then segmented row sums.

@@ -63,6 +63,7 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
   b += round_up(kpad32(k) * 4, 256);              // cn32f
   b += (size_t)TL_SEGS * TL_CAP * 8;  // tlist
   b += (size_t)TL_SEGS * 4;           // tcount
+  if (mind_ok(k, d)) b += round_up(k * MIND_LD * 4, 256);  // mind
   b += gemm_bytes(k, d);
   if (b1_ok(k, d)) {
     b += round_up(kpad32(k) * dpad16(d) * 2, 256);  // b1frag
@@ -106,6 +107,11 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   p += (size_t)TL_SEGS * TL_CAP * 8;
   v->tcount = (int32_t *)p;
   p += (size_t)TL_SEGS * 4;
+  v->mind = nullptr;
+  if (mind_ok(k, d)) {
+    v->mind = (float *)p;
+    p += round_up(k * MIND_LD * 4, 256);
+  }
   v->gfrag = nullptr;
   v->gfrag1 = nullptr;
   v->gcn = nullptr;
@@ -306,6 +312,40 @@ __global__ void __launch_bounds__(256) k_frag(const double *__restrict__ C,
   }
 }
 
+// Block-skip table of k_screen_b2 (IMG_SORTED): one block per centre p,
+// mind[p][cb] = a lower bound on min_{j in block cb, j != p, j < k}
+// |c_p - c_j|.  The fp64 distance is within (d + 4) 2^-53 of the true one
+// (d <= 128); 2^-40 and the fp32 round-down keep the stored value below it.
+// A NaN centre gives NaN entries, which never clear a block.
+__global__ void __launch_bounds__(256) k_mind(const double *__restrict__ C,
+                                              int64_t k, int64_t d,
+                                              float *__restrict__ mind) {
+  const int64_t p = blockIdx.x;
+  const int64_t nkb = (k + 31) / 32;
+  for (int64_t j0 = 0; j0 < nkb * 32; j0 += 256) {
+    const int64_t j = j0 + threadIdx.x;
+    double dist = INFINITY;
+    if (j < k && j != p) {
+      double a = 0.0;
+      for (int64_t t = 0; t < d; ++t) {
+        const double df = C[p * d + t] - C[j * d + t];
+        a = fma(df, df, a);
+      }
+      dist = sqrt(a) * (1.0 - 0x1.0p-40);
+    }
+    // min over the 32 lanes of the block (NaN-propagating)
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) {
+      const double o = __shfl_xor(dist, off, 32);
+      dist = (o != o || o < dist) ? o : dist;
+    }
+    if ((threadIdx.x & 31) == 0 && j < nkb * 32)
+      mind[p * MIND_LD + (j >> 5)] = __double2float_rd(dist);
+  }
+  for (int64_t cb = nkb + threadIdx.x; cb < MIND_LD; cb += 256)
+    mind[p * MIND_LD + cb] = INFINITY;
+}
+
 // ---------------------------------------------------------------------------
 // update: C[c] = sums/counts (counts != 0), per-centre shift, criterion
 // ---------------------------------------------------------------------------
@@ -455,6 +495,7 @@ int dkm_prepare_centers(const double *C, int64_t k, int64_t d, int flags,
     const int64_t g = std::max<int64_t>(1, std::min<int64_t>((tot + 255) / 256,
                                                             4096));
     k_frag<<<(unsigned)g, 256, 0, s>>>(C, k, d, v);
+    if (v.mind) k_mind<<<(unsigned)k, 256, 0, s>>>(C, k, d, v.mind);
   }
   if (int r = check_launch("dkm_prepare_centers")) return r;
   if (gemm_path(k, d) && !(flags & DKM_PREP_CSR))
@@ -505,6 +546,20 @@ int dkm_screen_stats(const void *ws, int64_t *n_rechecked, void *stream) {
     return fail((int)e, std::string("screen_stats: ") + hipGetErrorString(e));
   if (h.magic != WS_MAGIC) return fail(DKM_E_ARG, "screen_stats: bad ws");
   *n_rechecked = (int64_t)h.rechecked_total;
+  return 0;
+}
+
+int dkm_screen_counters(const void *ws, int64_t *out, void *stream) {
+  if (!ws || !out) return fail(DKM_E_ARG, "screen_counters: NULL");
+  WsHeader h;
+  hipError_t e = hipMemcpyAsync(&h, ws, sizeof(h), hipMemcpyDeviceToHost,
+                                (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  if (e != hipSuccess)
+    return fail((int)e, std::string("screen_counters: ") +
+                            hipGetErrorString(e));
+  if (h.magic != WS_MAGIC) return fail(DKM_E_ARG, "screen_counters: bad ws");
+  for (int i = 0; i < 3; ++i) out[i] = (int64_t)h.reserved[i];
   return 0;
 }
 

@@ -12,7 +12,7 @@ cd "$(dirname "$0")"
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
   d=build_$name; mkdir -p $d
-  for f in dkm_util dkm_dense dkm_b2 dkm_prune dkm_sparse dkm_gemm dkm_sums dkm_neighbors; do
+  for f in dkm_util dkm_dense dkm_b2 dkm_sparse dkm_gemm dkm_sums dkm_neighbors; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off \
       -fno-slp-vectorize $defs -c $f.hip -o $d/$f.o &
   done

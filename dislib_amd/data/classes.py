@@ -30,6 +30,21 @@ def _is_device_tensor(x):
     return type(x).__module__.startswith("torch") and hasattr(x, "is_cuda")
 
 
+def _freeze(x):
+    """Make a host sample array (or a CSR matrix's arrays) read-only: the
+    HBM copy is its image, so an in-place edit must fail loudly instead of
+    leaving later fits on stale device data (the reference re-reads the
+    samples on every task).  Assign a new array to change a Subset's
+    samples; that re-uploads."""
+    if isinstance(x, np.ndarray):
+        x.setflags(write=False)
+    elif issparse(x):
+        for a in (getattr(x, "data", None), getattr(x, "indices", None),
+                  getattr(x, "indptr", None)):
+            if isinstance(a, np.ndarray):
+                a.setflags(write=False)
+
+
 class _DeviceLabels:
     """Labels of a whole Dataset, resident on the device (int32)."""
 
@@ -236,9 +251,11 @@ class Dataset(object):
     def _signature(self):
         """Identity of the Subsets' sample objects: any reassignment
         (``ds[i].samples = ...``, ``Subset.concatenate``, a new Subset)
-        changes it.  In-place writes into a sample array keep it -- the
-        HBM image is then stale; re-assign the array to refresh it."""
-        return tuple((id(s.samples), tuple(s.samples.shape))
+        changes it, and so does an in-place write into a device tensor
+        (its ``_version`` counter).  Host arrays cannot change in place
+        unseen: they are made read-only once uploaded (``_freeze``)."""
+        return tuple((id(s.samples), tuple(s.samples.shape),
+                      getattr(s.samples, "_version", None))
                      for s in self._subsets)
 
     def _device_data(self, device=None):
@@ -257,6 +274,8 @@ class Dataset(object):
             dd = DeviceData(self, device)
             dd.signature = sig
             self._device = dd
+            for s in self._subsets:
+                _freeze(s.samples)
         return dd
 
     def _set_host_image(self, image):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define DKM_ABI_VERSION 1
+#define DKM_ABI_VERSION 2
 
 /* error codes (besides hipError_t values passed through) */
 #define DKM_OK 0
@@ -52,6 +52,15 @@ extern "C" {
                                a third of the matrix work, a looser bound;
                                the candidates it leaves are re-checked with
                                the EXACT arithmetic.  Labels identical.     */
+#define DKM_MODE_MASK 0xff  /* the arithmetic; flags may be OR'ed above it:  */
+#define DKM_MODE_NOHINT 0x100 /* the incoming labels of dkm_partial_sum /
+                               dkm_assign_delta are not used as hints (the
+                               caller knows them to be poor, e.g. labels of
+                               the initial centres): no threshold pass    */
+#define DKM_MODE_B1 0x200   /* the single-product screen in its
+                               centres-on-rows form (k_screen_b1, the
+                               fallback when k_screen_b2's LDS image does
+                               not fit) for every shape; identical labels */
 
 /* sum-dtype flags for dkm_update_centers (reference keeps X's dtype for the
  * partial sums; base.py:178 and :147) */
@@ -132,63 +141,57 @@ int dkm_assign_delta_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
 #define DKM_IMAGE_NONE 0
 #define DKM_IMAGE_SINGLE 1
 #define DKM_IMAGE_SPLIT 2
+#define DKM_IMAGE_SORTED 3
 int dkm_x_image_kind(int64_t k, int64_t d, int mode);
 size_t dkm_x_image_bytes(int64_t n, int64_t d, int kind);
 int dkm_x_image_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
                     int kind, void *image, size_t image_bytes, void *stream);
 int dkm_x_image_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
                     int kind, void *image, size_t image_bytes, void *stream);
+/* The label-sorted image (DKM_IMAGE_SORTED, dkm_x_image_bytes(n, d, 3)
+ * bytes): the DKM_IMAGE_SINGLE image of X with its rows grouped by
+ * `labels` (a counting sort in the workspace, which needs n label slots:
+ * dkm_workspace_bytes(k, d, n_queue >= n)), plus the row order and a copy of
+ * the labels in that order.  The single-product screen then screens 32-row
+ * tiles of (mostly) one label and skips every 32-centre block the triangle
+ * inequality proves farther than that label's centre.  The labels never
+ * depend on the grouping.  The image's label copy is maintained by the
+ * calls that take the image: once built, pass it to EVERY call that updates
+ * those labels (MODE_SCREEN_BF16 or AUTO; other modes refuse it), or build
+ * it again.  dkm_x_image_sorted_ok(k, d): whether (k, d) takes it.        */
+int dkm_x_image_sorted_ok(int64_t k, int64_t d);
+int dkm_x_image_sorted_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
+                           const int32_t *labels, int64_t k, const void *ws,
+                           size_t ws_bytes, void *image, size_t image_bytes,
+                           void *stream);
+int dkm_x_image_sorted_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
+                           const int32_t *labels, int64_t k, const void *ws,
+                           size_t ws_bytes, void *image, size_t image_bytes,
+                           void *stream);
+/* image_bytes: the image buffer's size, checked against
+ * dkm_x_image_bytes(n, d, image_kind) (an image built for other n or d is
+ * refused instead of read out of bounds).                                 */
 int dkm_partial_sum_img_f64(const double *X, const void *image, int image_kind,
-                            int64_t n, int64_t d, int64_t ldx,
-                            const double *C, int64_t k, const void *ws,
-                            size_t ws_bytes, int32_t *labels, double *acc,
-                            int mode, void *stream);
+                            size_t image_bytes, int64_t n, int64_t d,
+                            int64_t ldx, const double *C, int64_t k,
+                            const void *ws, size_t ws_bytes, int32_t *labels,
+                            double *acc, int mode, void *stream);
 int dkm_partial_sum_img_f32(const float *X, const void *image, int image_kind,
-                            int64_t n, int64_t d, int64_t ldx,
-                            const double *C, int64_t k, const void *ws,
-                            size_t ws_bytes, int32_t *labels, double *acc,
-                            int mode, void *stream);
+                            size_t image_bytes, int64_t n, int64_t d,
+                            int64_t ldx, const double *C, int64_t k,
+                            const void *ws, size_t ws_bytes, int32_t *labels,
+                            double *acc, int mode, void *stream);
 int dkm_assign_delta_img_f64(const double *X, const void *image,
-                             int image_kind, int64_t n, int64_t d,
+                             int image_kind, size_t image_bytes, int64_t n,
+                             int64_t d, int64_t ldx, const double *C,
+                             int64_t k, const void *ws, size_t ws_bytes,
+                             int32_t *labels, double *delta, int mode,
+                             void *stream);
+int dkm_assign_delta_img_f32(const float *X, const void *image, int image_kind,
+                             size_t image_bytes, int64_t n, int64_t d,
                              int64_t ldx, const double *C, int64_t k,
                              const void *ws, size_t ws_bytes, int32_t *labels,
                              double *delta, int mode, void *stream);
-int dkm_assign_delta_img_f32(const float *X, const void *image, int image_kind,
-                             int64_t n, int64_t d, int64_t ldx,
-                             const double *C, int64_t k, const void *ws,
-                             size_t ws_bytes, int32_t *labels, double *delta,
-                             int mode, void *stream);
-
-/* Bound-based skipping for the Lloyd loop (Hamerly-style triangle-inequality
- * bounds; dkm_prune.hip).  Same contract as dkm_assign_delta (labels in/out,
- * delta +=, identical labels), for the shapes dkm_prune_supported(k, d)
- * accepts (the single-product screen: d <= 128, d % 8 == 0, k x d within
- * LDS).  `state` (dkm_prune_state_bytes(n, k, d) bytes, caller-owned) holds
- * an upper bound on each sample's distance to its label and a lower bound on
- * its distance to every other centre.  init = 1 screens every sample and
- * (re)starts the bounds; init = 0 first moves the bounds by how far each
- * centre moved since the previous call (C_prev = the centres of that call,
- * k x d fp64) and screens only the samples whose bounds do not prove their
- * label unchanged, with margins that cover fp64 rounding of the distances.
- * The state is valid only across consecutive calls on the same X, labels
- * and a workspace prepared for C.  *n_active (host) receives the number of
- * samples screened; the call synchronizes `stream` once to read it.  image:
- * an optional DKM_IMAGE_SINGLE image (used when most samples are screened).
- * Replaces `_partial_sum`'s assignment (base.py:166-181) for the fit loop. */
-size_t dkm_prune_state_bytes(int64_t n, int64_t k, int64_t d);
-int dkm_prune_supported(int64_t k, int64_t d);
-int dkm_assign_pruned_f64(const double *X, const void *image, int image_kind,
-                          int64_t n, int64_t d, int64_t ldx, const double *C,
-                          const double *C_prev, int64_t k, const void *ws,
-                          size_t ws_bytes, int32_t *labels, double *delta,
-                          void *state, size_t state_bytes, int init,
-                          int64_t *n_active, void *stream);
-int dkm_assign_pruned_f32(const float *X, const void *image, int image_kind,
-                          int64_t n, int64_t d, int64_t ldx, const double *C,
-                          const double *C_prev, int64_t k, const void *ws,
-                          size_t ws_bytes, int32_t *labels, double *delta,
-                          void *state, size_t state_bytes, int init,
-                          int64_t *n_active, void *stream);
 
 /* acc[k*(d+1)] += [sums | counts] of the rows of X by labels (label < 0 or
  * >= k: skipped): the sums half of dkm_partial_sum for known labels.       */
@@ -305,6 +308,11 @@ int dkm_make_blobs_f64(double *X, int64_t row0, int64_t n, int64_t d,
 /* Diagnostics of the last SCREEN32 call on this workspace (device -> host,
  * synchronous on `stream`): number of samples sent to the exact re-check.  */
 int dkm_screen_stats(const void *ws, int64_t *n_rechecked, void *stream);
+/* Single-product screen counters over the workspace's life (host, syncs
+ * `stream`): out[0] tiles given the threshold pass, out[1] tiles it
+ * decided (the rest took the top-3 pass), out[2] 32-centre blocks screened
+ * by threshold passes over the label-sorted image (DKM_IMAGE_SORTED).     */
+int dkm_screen_counters(const void *ws, int64_t *out, void *stream);
 
 /* Build flags of this library: 0 for a product build.  Non-zero
  * (DKM_BUILD_TIMING_ONLY) when it was compiled with an A/B timing probe

