@@ -287,12 +287,13 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
     return out
 
 
-def traffic_for(n, d, k, path=None):
+def traffic_for(n, d, k, path=None, csr_nnz=0):
     """HBM bytes per assignment call from the committed PMC passes
     (tools/pmc_session.sh -> tools/pmc_summary.py --traffic-out): the
     per-sample read + write bytes of the screen and re-check kernels,
     scaled to n; None when no summary for this (d, k) is committed."""
     path = path or os.path.join(ROOT, "profiles", "traffic",
+                                ("csr%d_" % csr_nnz if csr_nnz else "") +
                                 "d%d_k%d.json" % (d, k))
     try:
         tj = json.load(open(path))
@@ -411,7 +412,35 @@ def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
                "fp64_peak_tflops": FP64_PEAK_TFLOPS,
                "hbm_gbs": n * es * d / sec / 1e9}
     out["traffic"] = None
+    out["binding"] = binding_for(d, k, csr_nnz)
     return out
+
+
+def binding_for(d, k, csr_nnz):
+    """The resource that actually limits the dominant kernel, from the PMC
+    passes committed under profiles/ (DESIGN.md 5): the algorithmic `frac`
+    prices fp64 X bytes or executed MFMA flops, which the screens that read
+    a resident bf16 image do not stream."""
+    if csr_nnz:
+        return ("L2 gather of the fp32 centre columns (4 B per stored entry "
+                "and centre; not HBM)")
+    if d > 128:
+        return "MFMA issue of the single-product bf16 GEMM screen"
+    return ("instruction issue (VALU + MFMA of the screen: neither the HBM "
+            "stream of the bf16 image nor the MFMA pipe saturates; "
+            "see `physical` and profiles/r04/pmc)")
+
+
+def physical(rf, n, sec):
+    """The HBM bytes the assignment kernels really move (PMC traffic per
+    launch) against the 8 TB/s peak, beside the algorithmic `frac`."""
+    tb = rf.get("traffic")
+    if not tb:
+        return None
+    return {"hbm_bytes_per_sample": tb / n, "achieved_gbs": tb / sec / 1e9,
+            "frac": tb / sec / 1e9 / HBM_PEAK_GBS,
+            "note": "PMC FETCH_SIZE x2 + WRITE_SIZE (gfx950 correction), "
+                    "profiles/traffic/"}
 
 
 def main():
@@ -510,10 +539,12 @@ def main():
              "steps": steps, "warmup": warm,
              "roofline": dict(roofline(n, d, k, rr, False, 4 if f32 else 8,
                                        csr_nnz=nnz),
-                              traffic=None if f32 or nnz else
-                              traffic_for(n, d, k)),
+                              traffic=None if f32 else
+                              traffic_for(n, d, k, csr_nnz=nnz)),
              "rechecked_samples": rr["rechecked"],
              "block_skip": skip_fields(rr)}
+        e["roofline"]["physical"] = physical(e["roofline"], n,
+                                             rr["kern_ms"] * 1e-3)
         e.update(fit_fields(rr, n, world))
         if nnz:
             e["nnz_per_row"] = nnz
@@ -542,6 +573,7 @@ def main():
     value = a.n * world * a.steps / r["el"]
     rf = roofline(a.n, a.d, a.k, r, a.labels)
     rf["traffic"] = traffic_for(a.n, a.d, a.k, a.traffic_json)
+    rf["physical"] = physical(rf, a.n, r["kern_ms"] * 1e-3)
     out = {
         "metric": METRIC,
         "value": value,

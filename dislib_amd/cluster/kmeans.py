@@ -165,6 +165,11 @@ REFRESH = int(os.environ.get("DKM_REFRESH", "64"))
 # (DKM_SORTED_IMAGE=0: A/B and parity runs).
 SORTED_IMAGE = os.environ.get("DKM_SORTED_IMAGE", "1") != "0"
 SORT_AT = 1
+# A/B knobs of the first two iterations (auto mode): the screen of iteration
+# 0 against the initial centres ("bf16x3" or the single product "bf16"), and
+# whether iteration 1 uses iteration 0's labels as hints ("0": top-3 pass)
+IT0_MODE = os.environ.get("DKM_IT0_MODE", "bf16x3")
+IT1_HINT = os.environ.get("DKM_IT1_HINT", "0") == "1"
 
 
 class _Lloyd:
@@ -254,14 +259,18 @@ class _Lloyd:
             # the first iteration scores against the initial centres, where
             # the single-product screen the library picks for large k x d
             # would leave most samples undecided -- screen it with bf16x3
-            mode = _lib.MODE_BF16X3
+            mode = _lib.MODE_BF16X3 if IT0_MODE == "bf16x3" else \
+                _lib.MODE_AUTO | _lib.MODE_NOHINT
+            if self.sorting:
+                image = (None, 0)
         elif self.sorting:
             if self.it <= SORT_AT:
                 # the labels of the initial centres are poor hints (most
                 # samples move): the top-3 pass directly, and no image yet
                 # (X is converted in the screen; the sorted image is built
                 # from this iteration's labels)
-                mode |= _lib.MODE_NOHINT
+                if not IT1_HINT:
+                    mode |= _lib.MODE_NOHINT
                 image = (None, 0)
             else:
                 image = self.simg or (None, 0)

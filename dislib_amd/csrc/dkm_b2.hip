@@ -74,8 +74,8 @@ constexpr int B2_RTHR = 4;   // over-full samples a wave tolerates per tile
 // [32][B2_ENT] reuse it after the tile's conversion), then 32 x nkw
 // own-mask words
 constexpr int B2_SCR_FIXED = 4 * 128 + 1024;
-static_assert(32 * B2_ENT * 8 + 256 <= 1024,
-              "kept entries, s_hat_p and the sample ids fit the transpose");
+static_assert(32 * B2_ENT * 8 + 128 <= 1024,
+              "kept entries and s_hat_p fit the transpose");
 
 // v_min3 / v_min without fminf's NaN canonicalisation (inline asm: the
 // compiler would insert v_max_f32 x, x on every MFMA result)
@@ -194,8 +194,6 @@ __global__ void __launch_bounds__(SB2)
   // VGPR too many: a spill reload whose vmcnt(0) waited for the prefetch);
   // the free tail of the transpose area, past the kept entries
   float *s_sp = (float *)(scr + 512 + 32 * B2_ENT * 8);
-  // SORTED: the rows' sample indices through the block loop (same reason)
-  int *s_sid = (int *)(scr + 512 + 32 * B2_ENT * 8 + 128);
   char *s_tx = scr + 512;                   // one K-step of the tile, bf16
   int2 *s_ent = (int2 *)(scr + 512);       // (score bits, centre), later
   uint32_t *s_om = (uint32_t *)(scr + B2_SCR_FIXED);  // [word][column]
@@ -402,38 +400,83 @@ __global__ void __launch_bounds__(SB2)
         // they can neither win nor tie (the margins cover the reference's
         // own fp64 rounding of both distances).  Rows that are not sane go
         // to the exact re-check whatever the blocks, so they do not count.
+        // A tile with a few hints (a label boundary of the sorted order, a
+        // sample that moved since the sort) takes the union over its hints
+        // q of the blocks that q's rows need: up to 4 hints, two at a time
+        // (lanes of half h test hint q_h, lane r block r) when nkb <= 32;
+        // with more hints every block is screened.
         uint64_t bmask = 0;
         if (SORTED) {
+          const bool rowok = sid >= 0 && sane0 && pok;
+          float u = 0.f;
+          if (rowok) {
+            const float u2 = fmaf(xx, 1.0f + 0x1.0p-16f, sp + B2t);
+            u = __builtin_sqrtf(fmaxf(u2, 0.f)) * (1.0f + 0x1.0p-20f);
+          }
           if (uni) {
-            float u = 0.f;
-            if (sid >= 0 && sane0) {
-              const float u2 = fmaf(xx, 1.0f + 0x1.0p-16f, sp + B2t);
-              u = __builtin_sqrtf(fmaxf(u2, 0.f)) * (1.0f + 0x1.0p-20f);
-            }
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1)
               u = fmaxf(u, __shfl_xor(u, off, 64));
             bmask = __ballot(lane < nkb && !(mnd > 2.0f * u));
+          } else if (v.mind) {
+            const int lpr = nkb <= 32 ? 2 : 1;  // hints per round
+            // rows still to cover (lanes 0..31 = rows; half 1 duplicates)
+            uint64_t todo = __ballot(h == 0 && rowok);
+            for (int rd = 0; rd < 4 && todo; rd += lpr) {
+              const int qa = __builtin_amdgcn_readlane(
+                  prv, (int)__builtin_ctzll(todo));
+              const uint64_t ma = __ballot(h == 0 && rowok && prv == qa);
+              todo &= ~ma;
+              int qb = qa;
+              uint64_t mb = 0;
+              if (lpr == 2 && todo) {
+                qb = __builtin_amdgcn_readlane(prv,
+                                               (int)__builtin_ctzll(todo));
+                mb = __ballot(h == 0 && rowok && prv == qb);
+                todo &= ~mb;
+              }
+              float ua = (ma >> r) & 1 ? u : 0.f;
+              float ub = (mb >> r) & 1 ? u : 0.f;
+#pragma unroll
+              for (int off = 16; off >= 1; off >>= 1) {
+                ua = fmaxf(ua, __shfl_xor(ua, off, 64));
+                ub = fmaxf(ub, __shfl_xor(ub, off, 64));
+              }
+              const bool second = lpr == 2 && h == 1;
+              const int q = second ? qb : qa;
+              const float U = second ? ub : ua;
+              const int cb = lpr == 2 ? r : lane;
+              const bool live = cb < nkb && (!second || mb != 0);
+              const float mn =
+                  live ? v.mind[(int64_t)q * MIND_LD + cb] : INFINITY;
+              const uint64_t nd = __ballot(live && !(mn > 2.0f * U));
+              bmask |= lpr == 2 ? ((nd & 0xffffffffull) | (nd >> 32)) : nd;
+            }
+            if (todo) bmask = nkb >= 64 ? ~0ull : ((1ull << nkb) - 1);
           } else {
             bmask = nkb >= 64 ? ~0ull : ((1ull << nkb) - 1);
           }
         }
         // ---- per-wave scratch: -T, hints, counts, own masks --------------
+        // (a uniform tile with one own-mask word per column needs no LDS
+        // mask: its only hinted centre is p0, column p0 & 31 of block
+        // p0 >> 5; nor the hints, nor the own block)
+        const bool fast_om = uni && W1;
         wave_sync();
         if (h == 0) {
           s_tn[r] = -T;
-          s_hp[r] = pok ? p : -1;
+          if (!uni) s_hp[r] = pok ? p : -1;
           s_cnt[r] = 0;
           s_sp[r] = sp;
         }
-        for (int w = lane; w < 32 * nkw; w += 64) s_om[w] = 0u;
-        wave_sync();
         uint32_t dup = 0;
-        if (h == 0 && pok) {
-          const uint32_t bit = 1u << ((p >> 5) & 31);
-          dup = atomicOr(&s_om[(p >> 10) * 32 + (p & 31)], bit) & bit;
-        }
-        {
+        if (!fast_om) {
+          for (int w = lane; w < 32 * nkw; w += 64) s_om[w] = 0u;
+          wave_sync();
+          if (h == 0 && pok) {
+            const uint32_t bit = 1u << ((p >> 5) & 31);
+            dup = atomicOr(&s_om[(p >> 10) * 32 + (p & 31)], bit) & bit;
+          }
           int da, db;
           pair_xor<32>((int)dup, da, db);
           dup = (uint32_t)(da | db);
@@ -444,17 +487,24 @@ __global__ void __launch_bounds__(SB2)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const f32x4 t4 = *(const f32x4 *)(s_tn + 8 * q + 4 * h);
-          const int4 p4 = *(const int4 *)(s_hp + 8 * q + 4 * h);
           cin[4 * q] = t4.x;
           cin[4 * q + 1] = t4.y;
           cin[4 * q + 2] = t4.z;
           cin[4 * q + 3] = t4.w;
-          pg[4 * q] = p4.x;
-          pg[4 * q + 1] = p4.y;
-          pg[4 * q + 2] = p4.z;
-          pg[4 * q + 3] = p4.w;
         }
-        const uint32_t om0 = s_om[r];
+        if (!uni) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int4 p4 = *(const int4 *)(s_hp + 8 * q + 4 * h);
+            pg[4 * q] = p4.x;
+            pg[4 * q + 1] = p4.y;
+            pg[4 * q + 2] = p4.z;
+            pg[4 * q + 3] = p4.w;
+          }
+        }
+        const uint32_t om0 =
+            fast_om ? (r == (p0 & 31) ? 1u << ((p0 >> 5) & 31) : 0u)
+                    : s_om[r];
         auto push = [&](int row, float s, int j) {
           const int slot = atomicAdd(&s_cnt[row], 1);
           if (slot < B2_ENT)
@@ -642,10 +692,21 @@ __global__ void __launch_bounds__(SB2)
         const int cnt = s_cnt[r];
         // the hint as the scratch holds it: p when usable, else -1 (a row
         // without a usable hint is `over`, so nothing below needs its
-        // incoming label)
-        prv = s_hp[(int)opaque_u32((uint32_t)r)];
+        // incoming label); a uniform tile's is p0
+        prv = uni ? p0 : s_hp[(int)opaque_u32((uint32_t)r)];
         const bool pokd = prv >= 0;
         const int pd = pokd ? prv : 0;
+        // steady state: no row kept a centre besides its hint, and every row
+        // is sane -- every label stays the hint: nothing to store or list
+        {
+          const float spq = s_sp[r];
+          const bool quick = pokd && sane0 && spq + B2t < 1e30f && cnt == 0;
+          if (__ballot(sid >= 0 && h == 0 && !quick) == 0) {
+            ++t_tiles;
+            ++t_done;
+            return;
+          }
+        }
         float sv[B2_ENT + 1];
         int cv[B2_ENT + 1];
         bool ok[B2_ENT + 1];

@@ -68,8 +68,7 @@ namespace {
 constexpr int CSR_BLOCK = 256;
 constexpr int CSR_G = 8;                   // lanes per sample
 constexpr int CSR_SPW = WAVE / CSR_G;      // samples per wave
-constexpr int CSR_PASS = 4 * CSR_G;        // centres per pass (4 per lane)
-constexpr size_t CSR_SLICE_BYTES = 2u << 20;  // fp32 C^T slice per XCD L2
+static_assert(CSR_PASS == 4 * CSR_G, "a pass is 4 centres per lane");
 constexpr int CSR_SEGP = 4096;             // sorted positions per sums block
 constexpr int CSR_TD = 16384;              // sums columns per LDS tile
 constexpr int CSR_SUMB = 1024;
@@ -106,7 +105,7 @@ __global__ void __launch_bounds__(CSR_BLOCK)
     k_csr_screen(const int64_t *__restrict__ indptr,
                  const int32_t *__restrict__ indices,
                  const double *__restrict__ data, int64_t i0, int64_t m,
-                 const float *__restrict__ CT, int64_t ldct,
+                 const float *__restrict__ CT, int64_t dct,
                  const float *__restrict__ cn, int k, int S, int ks,
                  SliceState *__restrict__ pst, int32_t *__restrict__ pidx,
                  float *__restrict__ pxx) {
@@ -117,6 +116,8 @@ __global__ void __launch_bounds__(CSR_BLOCK)
   const int64_t wv = stream * (CSR_BLOCK / 64) + (threadIdx.x >> 6);
   const int64_t nwv = nstream * (CSR_BLOCK / 64);
   const int j_lo = s * ks, j_hi = min(k, j_lo + ks);
+  // this slice's d x ks block of the sliced fp32 C^T
+  const float *CTs = CT + (int64_t)s * dct * ks - j_lo;
   for (int64_t q0 = wv * CSR_SPW; q0 < m; q0 += nwv * CSR_SPW) {
     const int64_t q = q0 + sg;
     const bool live = q < m;
@@ -148,7 +149,7 @@ __global__ void __launch_bounds__(CSR_BLOCK)
         for (int e = 0; e < CSR_G; ++e) {
           const int idx = __shfl(myi, gbase + e, WAVE);
           vv[e] = __shfl(myv, gbase + e, WAVE);
-          const float *row = CT + (int64_t)idx * ldct + jp + 4 * gl;
+          const float *row = CTs + (int64_t)idx * ks + jp + 4 * gl;
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
             const int j = jp + CSR_PASS * p + 4 * gl;
@@ -410,15 +411,6 @@ static int csr_cus() {
   return n;
 }
 
-// slices: the fewest (power of two <= 8) whose fp32 C^T slice fits the
-// budget, never narrower than one 32-centre pass
-static int csr_slices(int64_t k, int64_t d) {
-  int S = 1;
-  while (S < 8 && (k + S - 1) / S > CSR_PASS &&
-         (size_t)(round_up((k + S - 1) / S, CSR_PASS) * d * 4) > CSR_SLICE_BYTES)
-    S *= 2;
-  return S;
-}
 
 static int csr_full_sums(const int64_t *indptr, const int32_t *indices,
                          const double *data, int64_t n, int d, int k,
@@ -458,7 +450,7 @@ static int csr_run(const int64_t *indptr, const int32_t *indices,
   if (op == OP_FULL && (!labels || !sorted_sums_ok(k, 1, v)))
     op = OP_FULL_ATOMIC;  // no label array to sort (or k beyond the sort)
   const int S = csr_slices(k, d);
-  const int ks = (int)round_up((k + S - 1) / S, CSR_PASS);
+  const int ks = (int)csr_slice_width(k, d);
   // per chunk sample: S slice states (20 B), x.x bound (4 B), list slot (4 B)
   const int64_t chunk =
       std::min<int64_t>(n, v.nq * 12 / (20 * S + 8));
@@ -482,7 +474,7 @@ static int csr_run(const int64_t *indptr, const int32_t *indices,
     const unsigned g = (unsigned)(per_slice * S);
 #define DKM_SCREEN(NP)                                                       \
   k_csr_screen<NP><<<g, CSR_BLOCK, 0, st>>>(indptr, indices, data, i0, m,   \
-                                            v.ct32, ct_ld(k), v.cn32,       \
+                                            v.ct32, d, v.cn32,              \
                                             (int)k, S, ks, pst, pidx, pxx)
     if (npass >= 2)
       DKM_SCREEN(2);

@@ -2,12 +2,15 @@
 # Counter passes (rocprofv3 --pmc, kernel-trace only; never with sys/runtime
 # traces).  usage: bash tools/pmc_session.sh TAG TARGET
 #   TARGET = bench        -> bench.py on 20M rows (steady-state delta steps)
+#   TARGET = csr          -> tools/bench_csr.py (C5 CSR rows) on N rows
 #   TARGET = <mode list>  -> tools/bench_modes.py --modes <list> on 20M rows
 TAG=${1:-r01}; TARGET=${2:-bench}; shift 2
 OUT=gpurun_out/${TAG}_pmc; mkdir -p $OUT; export TMPDIR=/tmp
 N=${PMC_N:-20000000}
 if [ "$TARGET" = bench ]; then
   PROG=(python bench.py --n $N --steps 8 --warmup 4 --no-cpu --only-headline $BENCH_ARGS)
+elif [ "$TARGET" = csr ]; then
+  PROG=(python tools/bench_csr.py --n $N --steps 4 $BENCH_ARGS)
 else
   PROG=(python tools/bench_modes.py --n $N --rounds 2 --modes $TARGET)
 fi

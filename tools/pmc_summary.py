@@ -33,7 +33,7 @@ def load(d):
     return per
 
 
-ASSIGN = ("k_screen", "k_recheck", "k_cand", "k_gemm")
+ASSIGN = ("k_screen", "k_recheck", "k_cand", "k_gemm", "k_csr")
 
 
 def last_iteration_bytes(d):
