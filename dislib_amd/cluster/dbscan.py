@@ -113,25 +113,26 @@ def _compute_neighbours_csr(epsilon, min_samples, begin_idx, end_idx,
     return neigh, core
 
 
-def _concat_csr(subsets):
+def _concat_csr(subsets, who="compute_neighbours"):
     """The concatenated sparse samples as one CSR matrix with sorted column
-    indices (``_concatenate_subsets`` -> ``vstack``, classes.py:144-150)."""
+    indices (``_concatenate_subsets`` -> ``vstack``, classes.py:144-150).
+    Also the fit / query matrix of the sparse kNN (``who`` names the caller
+    in the errors)."""
     import scipy.sparse as sp
     if not subsets:
-        raise ValueError("compute_neighbours: no Subsets")
+        raise ValueError("%s: no Subsets" % who)
     parts = []
     for s in subsets:
         x = s.samples
         if not sp.issparse(x):
-            raise ValueError("compute_neighbours: sparse=True needs sparse "
-                             "Subsets")
+            raise ValueError("%s: sparse=True needs sparse Subsets" % who)
         parts.append(x)
     m = sp.csr_matrix(parts[0] if len(parts) == 1 else
                       sp.vstack(parts, format="csr"), dtype=np.float64)
     if not m.has_sorted_indices:
         m = m.sorted_indices()
     if m.shape[1] > np.iinfo(np.int32).max:
-        raise ValueError("compute_neighbours: too many features")
+        raise ValueError("%s: too many features" % who)
     # duplicate column entries in a row (legal while a scipy matrix is not
     # in canonical format): scipy's csr_matmat multiplies every stored pair
     # in stored order, which the kernel's merge of two sorted rows does not
@@ -144,8 +145,8 @@ def _concat_csr(subsets):
             row_start[m.indptr[:-1][np.diff(m.indptr) > 0]] = True
             if (same & ~row_start[1:]).any():
                 raise ValueError(
-                    "compute_neighbours: sparse samples hold duplicate "
-                    "column entries; call sum_duplicates() on them first")
+                    "%s: sparse samples hold duplicate column entries; call "
+                    "sum_duplicates() on them first" % who)
     _device_assert_finite(m.data)
     return m
 

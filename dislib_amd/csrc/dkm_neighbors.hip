@@ -21,6 +21,8 @@
 //   after the (r, index) where pass c - 1 ended (a per-query floor), so the
 //   passes enumerate the same (r, index) order, 32 entries at a time.
 //   Roofline: VALU fp64 -- 3 d ops (sub, mul, add) per pair.
+//   CSR Subsets: k_knn_csr_part, the same partitions and merge over the
+//   k_radius_csr intersection arithmetic (sklearn's brute force on CSR).
 //
 // * Epsilon query: DBSCAN _compute_neighbours (reference
 //   cluster/dbscan/classes.py:124-141): for each query row, every row with
@@ -58,26 +60,13 @@ struct TopK {
       i[s] = INT32_MAX;
     }
   }
-  // (v, j) with j larger than every index already held (scan order), so a
-  // strict < keeps the earlier index first among equal r; an empty slot
-  // (+inf, INT32_MAX) also takes a row at +inf (overflowed distance), so
-  // every list fills with real rows (sklearn returns them too)
-  __device__ __forceinline__ void push_seq(double v, int j) {
-    if (v < r[K - 1] || (v == r[K - 1] && i[K - 1] == INT32_MAX)) {
-#pragma unroll
-      for (int s = 0; s < K; ++s) {
-        const bool lt = v < r[s] || (v == r[s] && i[s] == INT32_MAX);
-        const double tr = r[s];
-        const int ti = i[s];
-        r[s] = lt ? v : tr;
-        i[s] = lt ? j : ti;
-        v = lt ? tr : v;
-        j = lt ? ti : j;
-      }
-    }
-  }
-  // arbitrary (v, j): lexicographic (r, index)
-  __device__ __forceinline__ void push_lex(double v, int j) {
+  // (v, j) by lexicographic (r, index).  The comparison stays lexicographic
+  // for the entry carried down the list after a swap: a displaced (r, i)
+  // must still go ahead of a held (r, i') with i < i' (a "strict <, empty
+  // slots take ties" rule for scan-order pushes drops it instead).  An empty
+  // slot (+inf, INT32_MAX) also takes a row at +inf (overflowed distance),
+  // so every list fills with real rows (sklearn returns them too).
+  __device__ __forceinline__ void push(double v, int j) {
     if (v < r[K - 1] || (v == r[K - 1] && j < i[K - 1])) {
 #pragma unroll
       for (int s = 0; s < K; ++s) {
@@ -146,13 +135,84 @@ __global__ void __launch_bounds__(NB)
     const int fi = live ? fli[q] : INT32_MAX;
     for (int64_t j = j0; j < j1; ++j) {
       const double r = seq_r<MAXD>(qv, qrow, xc + j * ldx, d);
-      if (r > fr || (r == fr && (int)j > fi)) top.push_seq(r, (int)j);
+      if (r > fr || (r == fr && (int)j > fi)) top.push(r, (int)j);
     }
   } else {
     for (int64_t j = j0; j < j1; ++j) {
       const double r = seq_r<MAXD>(qv, qrow, xc + j * ldx, d);
-      top.push_seq(r, (int)j);
+      top.push(r, (int)j);
     }
+  }
+  if (!live) return;
+  double *po = pr + (q * P + p) * K;
+  int *io = pi + (q * P + p) * K;
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    po[s] = top.r[s];
+    io[s] = top.i[s];
+  }
+}
+
+// Sparse kNN partial lists.  sklearn picks brute force for CSR fit data and,
+// its ArgKmin reduction refusing sparse-sparse pairs, ranks by
+// pairwise_distances_chunked(squared=True): r = max(((-2 q.x) + ||q||^2) +
+// ||x||^2, 0) in the arithmetic of k_radius_csr below (row norms summed in
+// stored order, q.x in the query's stored = increasing-column order), then
+// sqrt(r).  The self pair is exactly 0 (q.q and ||q||^2 are the same sum).
+// lane = query row (its merge cursor), wave-uniform fit row j (scalar
+// loads), fit rows partitioned over blockIdx.y like k_knn_part.
+template <int K>
+__global__ void __launch_bounds__(NB)
+    k_knn_csr_part(const int64_t *__restrict__ qp,
+                   const int32_t *__restrict__ qi,
+                   const double *__restrict__ qd, int64_t nq,
+                   const int64_t *__restrict__ xp,
+                   const int32_t *__restrict__ xi,
+                   const double *__restrict__ xd, int64_t nx, int64_t plen,
+                   int P, double *__restrict__ pr, int *__restrict__ pi,
+                   const double *__restrict__ flr,
+                   const int *__restrict__ fli) {
+  const int lane = threadIdx.x & 63;
+  const int64_t qg = (int64_t)blockIdx.x * (NB / 64) +
+                     __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int p = blockIdx.y;
+  const int64_t q = qg * 64 + lane;
+  if (qg * 64 >= nq) return;  // wave-uniform
+  const bool live = q < nq;
+  const int64_t qa = live ? qp[q] : 0;
+  const int64_t qb = live ? qp[q + 1] : 0;
+  double xx = 0.0;
+  for (int64_t t = qa; t < qb; ++t) {
+    const double v = qd[t];
+    xx += v * v;
+  }
+  const double fr = (live && flr) ? flr[q] : -INFINITY;
+  const int fi = (live && fli) ? fli[q] : -1;
+  TopK<K> top;
+  top.init();
+  const int64_t j0 = (int64_t)p * plen;
+  const int64_t j1 = std::min<int64_t>(nx, j0 + plen);
+  for (int64_t j = j0; j < j1; ++j) {
+    const int64_t a = xp[j], b = xp[j + 1];
+    double yy = 0.0, dot = 0.0;
+    int64_t t = qa;
+    int32_t qc = t < qb ? qi[t] : INT32_MAX;
+    for (int64_t u = a; u < b; ++u) {
+      const int32_t c = xi[u];
+      const double v = xd[u];
+      yy += v * v;
+      while (qc < c) {
+        ++t;
+        qc = t < qb ? qi[t] : INT32_MAX;
+      }
+      if (qc == c) dot += qd[t] * v;
+    }
+    double r = -2.0 * dot;
+    r += xx;
+    r += yy;
+    r = r < 0.0 ? 0.0 : r;
+    // a later pass: only (r, j) strictly after the previous pass's last
+    if (r > fr || (r == fr && (int)j > fi)) top.push(r, (int)j);
   }
   if (!live) return;
   double *po = pr + (q * P + p) * K;
@@ -181,7 +241,7 @@ __global__ void __launch_bounds__(NB)
       const double v = a[s];
       if (!(v < top.r[K - 1]) && !(v == top.r[K - 1] && b[s] < top.i[K - 1]))
         break;  // the partition's list is sorted: nothing further enters
-      top.push_lex(v, b[s]);
+      top.push(v, b[s]);
     }
   }
 #pragma unroll
@@ -505,6 +565,34 @@ int knn_dispatch(int maxd, dim3 g, hipStream_t s, const double *Q, int64_t nq,
   return check_launch("knn partial lists");
 }
 
+template <int K>
+int knn_csr_launch(dim3 g, hipStream_t s, const int64_t *qp,
+                   const int32_t *qi, const double *qd, int64_t nq,
+                   const int64_t *xp, const int32_t *xi, const double *xd,
+                   int64_t nx, int64_t plen, int P, double *pr, int *pi,
+                   const double *flr, const int *fli) {
+  k_knn_csr_part<K><<<g, NB, 0, s>>>(qp, qi, qd, nq, xp, xi, xd, nx, plen, P,
+                                     pr, pi, flr, fli);
+  return check_launch("knn csr partial lists");
+}
+
+// the merge of one pass (K = slots of the partial lists, kk <= K columns
+// of out starting at c0)
+int knn_merge_launch(int K, hipStream_t s, const double *pr, const int *pi,
+                     int64_t nq, int P, int kk, double *od, int64_t *oi,
+                     int64_t ldo, double *flr, int *fli) {
+  const unsigned gm = (unsigned)((nq + NB - 1) / NB);
+  switch (K) {
+    case 1: k_knn_merge<1><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
+    case 2: k_knn_merge<2><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
+    case 4: k_knn_merge<4><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
+    case 8: k_knn_merge<8><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
+    case 16: k_knn_merge<16><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
+    default: k_knn_merge<32><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
+  }
+  return check_launch("knn merge");
+}
+
 int knn_args(const double *Q, int64_t nq, int64_t ldq, const double *X,
              int64_t nx, int64_t ldx, int64_t d, int64_t kn) {
   if (nq < 0 || nx < 1 || d < 1 || ldq < d || ldx < d)
@@ -606,7 +694,6 @@ int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
   int *fli = (int *)(flr + nq);
   const dim3 g((unsigned)((nq + 255) / 256), (unsigned)P);
   const int maxd = maxd_of(d);
-  const unsigned gm = (unsigned)((nq + NB - 1) / NB);
   for (int64_t c0 = 0; c0 < kn; c0 += 32) {
     const int kk = (int)std::min<int64_t>(32, kn - c0);
     const int K = knn_k(kk);
@@ -622,17 +709,61 @@ int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
       default: r = knn_dispatch<32>(maxd, g, s, Q, nq, ldq, X, nx, ldx, (int)d, plen, P, pr, pi, fr, fi); break;
     }
     if (r) return r;
-    double *od = out_dist + c0;
-    int64_t *oi = out_idx + c0;
+    if (int e = knn_merge_launch(K, s, pr, pi, nq, P, kk, out_dist + c0,
+                                 out_idx + c0, kn, flr, fli))
+      return e;
+  }
+  return 0;
+}
+
+int dkm_knn_csr_f64(const int64_t *q_indptr, const int32_t *q_indices,
+                    const double *q_data, int64_t nq, const int64_t *x_indptr,
+                    const int32_t *x_indices, const double *x_data,
+                    int64_t nx, int64_t d, int64_t kn, void *ws,
+                    size_t ws_bytes, double *out_dist, int64_t *out_idx,
+                    void *stream) {
+  if (nq < 0 || nx < 1 || d < 1 || d > INT32_MAX || nx > INT32_MAX)
+    return fail(DKM_E_ARG, "knn csr: bad nq/nx/d");
+  if (kn < 1 || kn > nx)
+    return fail(DKM_E_ARG, "knn csr: n_neighbors must be in [1, nx]");
+  if (nq == 0) return 0;
+  if (!q_indptr || !q_indices || !q_data || !x_indptr || !x_indices ||
+      !x_data)
+    return fail(DKM_E_ARG, "knn csr: NULL indptr/indices/data");
+  if (!out_dist || !out_idx) return fail(DKM_E_ARG, "knn csr: NULL outputs");
+  const size_t need = dkm_knn_workspace_bytes(nq, nx, kn);
+  if (!ws || ws_bytes < need)
+    return fail(DKM_E_WORKSPACE, "knn csr: workspace smaller than "
+                                 "dkm_knn_workspace_bytes()");
+  hipStream_t s = (hipStream_t)stream;
+  int64_t plen;
+  int P;
+  knn_grid(nq, nx, &plen, &P);
+  const int KP = knn_k(std::min<int64_t>(kn, 32));
+  double *pr = (double *)ws;
+  int *pi = (int *)(pr + (size_t)nq * P * KP);
+  double *flr = (double *)(((uintptr_t)(pi + (size_t)nq * P * KP) + 255) &
+                           ~(uintptr_t)255);
+  int *fli = (int *)(flr + nq);
+  const dim3 g((unsigned)((nq + 255) / 256), (unsigned)P);
+  for (int64_t c0 = 0; c0 < kn; c0 += 32) {
+    const int kk = (int)std::min<int64_t>(32, kn - c0);
+    const int K = knn_k(kk);
+    const double *fr = c0 ? flr : nullptr;
+    const int *fi = c0 ? fli : nullptr;
+    int r;
     switch (K) {
-      case 1: k_knn_merge<1><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
-      case 2: k_knn_merge<2><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
-      case 4: k_knn_merge<4><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
-      case 8: k_knn_merge<8><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
-      case 16: k_knn_merge<16><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
-      default: k_knn_merge<32><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, kn, flr, fli); break;
+      case 1: r = knn_csr_launch<1>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
+      case 2: r = knn_csr_launch<2>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
+      case 4: r = knn_csr_launch<4>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
+      case 8: r = knn_csr_launch<8>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
+      case 16: r = knn_csr_launch<16>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
+      default: r = knn_csr_launch<32>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
     }
-    if (int e = check_launch("knn merge")) return e;
+    if (r) return r;
+    if (int e = knn_merge_launch(K, s, pr, pi, nq, P, kk, out_dist + c0,
+                                 out_idx + c0, kn, flr, fli))
+      return e;
   }
   return 0;
 }

@@ -19,7 +19,17 @@ Differences from the reference (documented, not reproduced):
 * ``n_neighbors`` beyond 32 runs in passes of 32 columns (the kernel's
   register-resident top-k), each starting after the previous pass's last
   (distance, index).
-* Sparse Subsets are not supported on this path.
+* Sparse Subsets: sklearn fits brute force on CSR and ranks by
+  ``pairwise_distances_chunked(squared=True)`` (its ArgKmin reduction
+  refuses sparse-sparse pairs): ``dkm_knn_csr_f64`` computes the same
+  ``((-2 q.x) + ||q||^2) + ||x||^2`` in the same order (the sparse epsilon
+  query's arithmetic), so the distances are bit-exact; rows are read with
+  sorted column indices, and a row holding a duplicate column is refused.
+  A dense query against sparse fit data (or the reverse) raises ValueError:
+  the reference's kd_tree refuses the one, and the other takes a
+  dense-times-sparse product whose order is scipy's, not pinned here.
+* Ties: the reference merges with ``np.argsort`` (quicksort, unstable);
+  here equal distances come out by ascending fit row.
 """
 import ctypes
 import numbers
@@ -64,8 +74,11 @@ class NearestNeighbors:
             raise ValueError("NearestNeighbors: call fit() first")
         _check_n_neighbors(n_neighbors, self._fit_dataset)
         if dataset.sparse or self._fit_dataset.sparse:
-            raise ValueError("NearestNeighbors: sparse Subsets are not "
-                             "supported by the GPU path")
+            if not (dataset.sparse and self._fit_dataset.sparse):
+                raise ValueError("NearestNeighbors: the query and the fitted "
+                                 "Dataset must both be sparse or both dense")
+            return self._kneighbors_csr(dataset, n_neighbors,
+                                        return_distance)
         t = torch()
         fit_dd = self._fit_dataset._device_data(self._device)
         q_dd = dataset._device_data(fit_dd.device)
@@ -92,6 +105,56 @@ class NearestNeighbors:
             if not return_distance:
                 return ind
             return out_d.cpu().numpy(), ind
+
+
+    def _kneighbors_csr(self, dataset, n_neighbors, return_distance):
+        """CSR Subsets: both Datasets concatenated to one CSR matrix each
+        (sorted indices, finite, no duplicate columns) and ranked by
+        ``dkm_knn_csr_f64``."""
+        from ..cluster.dbscan import _concat_csr
+        from .._device import resolve
+        t = torch()
+        xf = _concat_csr(list(self._fit_dataset), "NearestNeighbors")
+        same = dataset is self._fit_dataset
+        xq = xf if same else _concat_csr(list(dataset), "NearestNeighbors")
+        nq, nx, d = xq.shape[0], xf.shape[0], xf.shape[1]
+        if xq.shape[1] != d:
+            raise ValueError("X has %d features, but NearestNeighbors is "
+                             "expecting %d features as input"
+                             % (xq.shape[1], d))
+        dev = resolve(self._device)
+        so = _lib.lib()
+        with on(dev):
+            f = _csr_to(xf, dev)
+            q = f if same else _csr_to(xq, dev)
+            out_d = t.empty((nq, n_neighbors), dtype=t.float64, device=dev)
+            out_i = t.empty((nq, n_neighbors), dtype=t.int64, device=dev)
+            if nq:
+                wsb = int(so.dkm_knn_workspace_bytes(nq, nx, n_neighbors))
+                ws = t.empty(max(wsb, 1), dtype=t.uint8, device=dev)
+                _lib.check(so.dkm_knn_csr_f64(
+                    ptr(q[0]), ptr(q[1]), ptr(q[2]), nq, ptr(f[0]),
+                    ptr(f[1]), ptr(f[2]), nx, d, n_neighbors,
+                    ctypes.c_void_p(ws.data_ptr()), wsb, ptr(out_d),
+                    ptr(out_i), stream_ptr()), "dkm_knn_csr_f64")
+            ind = out_i.cpu().numpy()
+            if not return_distance:
+                return ind
+            return out_d.cpu().numpy(), ind
+
+
+def _csr_to(m, dev):
+    """(indptr int64, indices int32, data fp64) device tensors of a CSR
+    matrix (one-element arrays for an all-zero matrix, so every pointer is
+    a valid device address)."""
+    t = torch()
+    indptr = t.from_numpy(m.indptr.astype(np.int64)).to(dev)
+    indices = np.ascontiguousarray(m.indices, dtype=np.int32)
+    data = np.ascontiguousarray(m.data, dtype=np.float64)
+    if data.size == 0:
+        indices = np.zeros(1, np.int32)
+        data = np.zeros(1, np.float64)
+    return indptr, t.from_numpy(indices).to(dev), t.from_numpy(data).to(dev)
 
 
 def _as_f64(x):

@@ -341,6 +341,21 @@ int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
                 int64_t nx, int64_t ldx, int64_t d, int64_t kn, void *ws,
                 size_t ws_bytes, double *out_dist, int64_t *out_idx,
                 void *stream);
+/* Sparse kNN, replacing the same reference path on CSR Subsets (sklearn
+ * fits brute force on CSR and ranks by pairwise_distances_chunked with
+ * squared=True): query CSR (q_indptr[nq+1] int64, q_indices int32 sorted
+ * and unique within each row, q_data fp64) against the fit CSR (nx rows),
+ * both d columns.  r = max(((-2 q.x) + ||q||^2) + ||x||^2, 0) in the
+ * arithmetic of dkm_radius_count_csr_f64; neighbours ascending (r, index),
+ * out_dist = sqrt(r).  kn in [1, nx] (passes of 32 beyond 32); workspace =
+ * dkm_knn_workspace_bytes(nq, nx, kn).  The query and fit matrices may be
+ * the same arrays. */
+int dkm_knn_csr_f64(const int64_t *q_indptr, const int32_t *q_indices,
+                    const double *q_data, int64_t nq, const int64_t *x_indptr,
+                    const int32_t *x_indices, const double *x_data,
+                    int64_t nx, int64_t d, int64_t kn, void *ws,
+                    size_t ws_bytes, double *out_dist, int64_t *out_idx,
+                    void *stream);
 
 /* DBSCAN epsilon query, replacing _compute_neighbours (dense) of
  * dislib/cluster/dbscan/classes.py:124-141: for query row q, the rows j of

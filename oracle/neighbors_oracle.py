@@ -155,11 +155,21 @@ def csr_sq_distances(indptr, indices, data, q):
     from 0 in q's stored order), ``D += XX``, ``D += YY``,
     ``np.maximum(D, 0)``."""
     indptr = np.asarray(indptr, np.int64)
+    qa, qb = indptr[q], indptr[q + 1]
+    return csr_sq_distances_to(np.asarray(indices)[qa:qb],
+                               np.asarray(data, np.float64)[qa:qb],
+                               indptr, indices, data)
+
+
+def csr_sq_distances_to(qi, qv, indptr, indices, data, yy=None):
+    """:func:`csr_sq_distances` of a query row given by its sorted column
+    indices ``qi`` and values ``qv`` against every row of the CSR matrix
+    (``yy``: its precomputed stored-order row norms, optional)."""
+    indptr = np.asarray(indptr, np.int64)
     indices = np.asarray(indices)
     data = np.asarray(data, np.float64)
-    yy = _seq_row_sums(indptr, data * data)
-    qa, qb = indptr[q], indptr[q + 1]
-    qi, qv = indices[qa:qb], data[qa:qb]
+    if yy is None:
+        yy = _seq_row_sums(indptr, data * data)
     xx = 0.0
     for v in qv:
         xx += v * v
@@ -184,6 +194,32 @@ def csr_sq_distances(indptr, indices, data, q):
     r += xx
     r += yy
     return np.maximum(r, 0.0)
+
+
+def kneighbors_csr(f_csr, q_csr, n_neighbors):
+    """Sparse ``kneighbors`` (reference neighbors/base.py:40-111 on CSR
+    Subsets): sklearn fits brute force on CSR and ranks by
+    ``pairwise_distances_chunked(squared=True)`` -- the squared distances of
+    :func:`csr_sq_distances_to` -- then reports ``sqrt``.  ``f_csr`` /
+    ``q_csr`` = (indptr, indices, data) with sorted indices.  Returns
+    ``(dist, ind)`` ascending by (squared distance, fit row); the
+    reference's argpartition / argsort order equal distances arbitrarily."""
+    fp, fi, fd = (np.asarray(a) for a in f_csr)
+    qp, qi, qd = (np.asarray(a) for a in q_csr)
+    fd = fd.astype(np.float64)
+    yy = _seq_row_sums(fp.astype(np.int64), fd * fd)
+    nq = qp.size - 1
+    dist = np.empty((nq, n_neighbors))
+    ind = np.empty((nq, n_neighbors), np.int64)
+    rows = np.arange(fp.size - 1)
+    for q in range(nq):
+        a, b = qp[q], qp[q + 1]
+        r = csr_sq_distances_to(qi[a:b], qd[a:b].astype(np.float64), fp, fi,
+                                fd, yy)
+        o = np.lexsort((rows, r))[:n_neighbors]
+        dist[q] = np.sqrt(r[o])
+        ind[q] = o
+    return dist, ind
 
 
 def compute_neighbours_csr(epsilon, min_samples, begin_idx, end_idx,

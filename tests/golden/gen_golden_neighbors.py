@@ -15,7 +15,7 @@ imports the reference under the sequential PyCOMPSs stub.  Nothing of the
 reference is copied: inputs are seeded synthetic matrices (stored, they are
 small), outputs are what the reference returned.  Writes
 ``neighbors_ref.npz`` and ``neighbors_sparse_ref.npz`` (the epsilon query
-on sparse Subsets).
+and kneighbors on sparse Subsets).
 """
 import os
 import subprocess
@@ -50,6 +50,15 @@ DB_SPARSE_CASES = [
     ("dbs_wide", 300, 2000, 100, 0.005, 2.3, 2, 20, 280),   # ~10 nnz / row
     ("dbs_empty", 150, 30, 50, 0.03, 0.3, 2, 0, 150),       # empty rows
     ("dbs_blobs", 240, 20, 60, None, 5.5, 4, 30, 210),      # thresholded blobs
+]
+# sparse kneighbors (sklearn brute force on CSR):
+# (name, n_fit, n_query or None (query = fit), d, subset, density, n_neighbors)
+KNN_SPARSE_CASES = [
+    ("kns_small", 200, None, 50, 50, 0.1, 5),
+    ("kns_wide", 300, None, 2000, 100, 0.005, 8),   # mostly disjoint rows
+    ("kns_empty", 150, None, 30, 50, 0.03, 4),      # empty rows: ties at 0
+    ("kns_other", 240, 120, 20, 60, None, 6),       # queries != fit data
+    ("kns_40", 400, None, 30, 100, 0.2, 40),        # > 32: two passes
 ]
 
 
@@ -123,6 +132,35 @@ def generate():
         out[name + "__core"] = np.asarray(cp, dtype=bool)
         print("dbscan sparse", name, x.nnz, "nnz", int(lens.sum()),
               "neighbours")
+    for i, (name, nf, nq, d, sub, dens, kn) in enumerate(KNN_SPARSE_CASES):
+        rng = np.random.default_rng(400 + i)
+
+        def _csr(n):
+            if dens is None:
+                x = _data(rng, n, d, "blobs")
+                x[np.abs(x) < 1.0] = 0.0
+                x = sp.csr_matrix(x)
+            else:
+                x = sp.random(n, d, density=dens, format="csr",
+                              random_state=rng,
+                              data_rvs=lambda k: rng.uniform(-1, 1, k))
+            x.sort_indices()
+            return x
+        xf = _csr(nf)
+        xq = xf if nq is None else _csr(nq)
+        knn = NearestNeighbors(n_neighbors=kn)
+        fds = load_data(xf, subset_size=sub)
+        knn.fit(fds)
+        dist, ind = knn.kneighbors(fds if nq is None else
+                                   load_data(xq, subset_size=sub))
+        for tag, x in (("f", xf), ("q", xq)):
+            out["%s__%sindptr" % (name, tag)] = x.indptr.astype(np.int64)
+            out["%s__%sindices" % (name, tag)] = x.indices.astype(np.int32)
+            out["%s__%sdata" % (name, tag)] = x.data
+        out[name + "__meta"] = np.array([sub, kn, d], dtype=np.int64)
+        out[name + "__dist"] = np.asarray(dist)
+        out[name + "__ind"] = np.asarray(ind)
+        print("kneighbors sparse", name, np.asarray(dist).shape)
     np.savez_compressed(os.path.join(HERE, "neighbors_sparse_ref.npz"), **out)
     print("wrote neighbors_sparse_ref.npz")
 

@@ -87,6 +87,23 @@ def test_kneighbors_ties_by_index():
     assert np.array_equal(ind, oi) and np.array_equal(dist, od)
 
 
+def test_kneighbors_closer_row_after_a_full_tie_group():
+    """A full list of equal distances, then a closer row: the displaced
+    entries carried down the list keep their index order, so the lowest
+    index of the tie group survives (an insertion that only let empty slots
+    take ties dropped it: [10, 1, 2, 3] instead of [10, 0, 1, 2])."""
+    xf = np.zeros((40, 2))
+    xf[:10, 0] = 1.0           # rows 0..9 at distance 1
+    xf[10] = 0.0               # row 10 at distance 0
+    xf[11:] = 5.0 + np.arange(29)[:, None]
+    xq = np.zeros((3, 2))
+    dist, ind = _knn(xf, xq, 40, 4, 3)
+    assert ind.tolist() == [[10, 0, 1, 2]] * 3
+    assert dist.tolist() == [[0.0, 1.0, 1.0, 1.0]] * 3
+    od, oi = orc.kneighbors_exact(xf, xq, 4)
+    assert np.array_equal(ind, oi)
+
+
 def test_kneighbors_overflowed_distances_fill_the_list():
     """Fewer finite rows than n_neighbors: rows whose squared distance
     overflows to +inf still fill the list (sklearn returns them too), as
@@ -230,3 +247,102 @@ def test_sparse_epsilon_query_vs_oracle(n, d, dens, eps, b, e, kind):
     assert cp == ocp
     if kind == "grid" and eps > 0:
         assert sum(len(v) for v in nl) > n  # more than the points themselves
+
+
+# --- sparse kneighbors (sklearn brute force on CSR Subsets) ---------------
+from tests.test_neighbors_golden import (KNS, assert_knn_same_up_to_ties,  # noqa
+                                         sp_matrix, sparse_knn_case)
+
+
+def _knn_csr(mf, mq, sub, kn, subq=None, same=False):
+    from dislib_amd.data import load_data
+    from dislib_amd.neighbors import NearestNeighbors
+    nn = NearestNeighbors(n_neighbors=kn)
+    fds = load_data(mf, subset_size=sub)
+    nn.fit(fds)
+    return nn.kneighbors(fds if same else load_data(mq, subset_size=subq or sub))
+
+
+@pytest.mark.parametrize("name", KNS)
+def test_sparse_kneighbors_reference_golden(name):
+    """Distances bit-exact against what the reference returned; indices
+    equal up to the order of exactly equal distances."""
+    f, q, d, sub, kn, dist, ind = sparse_knn_case(name)
+    mf, mq = sp_matrix(f, d), sp_matrix(q, d)
+    same = np.array_equal(f[0], q[0]) and np.array_equal(f[2], q[2]) and \
+        np.array_equal(f[1], q[1])
+    gd, gi = _knn_csr(mf, mq, sub, kn, same=same)
+    assert gi.dtype == np.int64 and gd.dtype == np.float64
+    assert_knn_same_up_to_ties(gd, gi, dist, ind, name)
+    od, oi = orc.kneighbors_csr(f, q, kn)
+    assert np.array_equal(gi, oi) and np.array_equal(gd, od)
+
+
+@pytest.mark.parametrize("nq,nx,d,dens,kn,kind", [
+    (3000, 5000, 500, 0.02, 5, "uniform"),     # many partitions
+    (1000, 8000, 50, 0.1, 32, "uniform"),      # the largest single pass
+    (500, 3000, 8, 0.5, 40, "grid"),           # ties on integers, 2 passes
+    (700, 2000, 100000, 0.00001, 6, "uniform"),  # ~37% empty rows: ties
+    (129, 300, 30, 0.2, 1, "uniform"),         # ragged wave, one neighbour
+    (300, 1500, 20, 0.3, 70, "big"),           # 1e200 entries: inf rows
+    (256, 600, 40, 0.2, 9, "unsorted"),        # unsorted rows read sorted
+])
+def test_sparse_kneighbors_vs_oracle(nq, nx, d, dens, kn, kind):
+    import scipy.sparse as sp
+    rng = np.random.default_rng(nq + nx + d)
+    rvs = {"grid": lambda k: rng.integers(1, 4, k).astype(np.float64),
+           "big": lambda k: rng.choice([1.0, -2.0, 1e200], k,
+                                       p=[0.45, 0.45, 0.1])}.get(
+        kind, lambda k: rng.uniform(-1, 1, k))
+    mf = sp.random(nx, d, density=dens, format="csr", random_state=rng,
+                   data_rvs=rvs)
+    mq = sp.random(nq, d, density=dens, format="csr", random_state=rng,
+                   data_rvs=rvs)
+    mf.sort_indices()
+    mq.sort_indices()
+    f = (mf.indptr.astype(np.int64), mf.indices, mf.data)
+    q = (mq.indptr.astype(np.int64), mq.indices, mq.data)
+    if kind == "unsorted":
+        ip = mf.indptr
+        perm = np.concatenate([np.arange(ip[i + 1] - 1, ip[i] - 1, -1)
+                               for i in range(nx)]).astype(np.int64)
+        mf = sp.csr_matrix((mf.data[perm], mf.indices[perm], ip),
+                           shape=mf.shape)
+        assert not mf.has_sorted_indices
+    gd, gi = _knn_csr(mf, mq, 1000, kn, 250)
+    od, oi = orc.kneighbors_csr(f, q, kn)
+    if kind == "big":
+        # NaN squared distances (inf - inf) never enter a list here; the
+        # oracle ranks them last: compare where the oracle's are not NaN
+        ok = ~np.isnan(od).any(1)
+        assert ok.sum() > nq // 2
+        gd, gi, od, oi = gd[ok], gi[ok], od[ok], oi[ok]
+    assert np.array_equal(gi, oi)
+    assert np.array_equal(gd, od)
+
+
+def test_sparse_kneighbors_self_query_is_zero_and_errors():
+    """Querying the fitted Dataset itself: every row's first neighbour is
+    itself at distance exactly 0 (q.q and ||q||^2 are the same sum); mixed
+    dense / sparse Datasets and duplicate column entries raise."""
+    import scipy.sparse as sp
+    from dislib_amd.data import load_data
+    from dislib_amd.neighbors import NearestNeighbors
+    rng = np.random.default_rng(3)
+    m = sp.random(400, 60, density=0.2, format="csr", random_state=rng)
+    m = m + sp.random(400, 60, density=0.0, format="csr")   # canonical
+    m.data = rng.standard_normal(m.nnz) * 7.0
+    nn = NearestNeighbors(n_neighbors=3)
+    ds = load_data(m.tocsr(), subset_size=100)
+    nn.fit(ds)
+    dist, ind = nn.kneighbors(ds)
+    nz = np.diff(m.indptr) > 0
+    assert np.all(dist[:, 0] == 0.0)
+    assert np.array_equal(ind[nz, 0], np.nonzero(nz)[0])
+    with pytest.raises(ValueError, match="both be sparse or both dense"):
+        nn.kneighbors(load_data(m.toarray(), subset_size=100))
+    dup = sp.csr_matrix((np.array([1.0, 2.0, 3.0]), np.array([0, 0, 1]),
+                         np.array([0, 2, 3])), shape=(2, 4))
+    nn.fit(load_data(dup, subset_size=2))
+    with pytest.raises(ValueError, match="duplicate column"):
+        nn.kneighbors(load_data(dup, subset_size=2), n_neighbors=1)

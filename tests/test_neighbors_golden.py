@@ -69,7 +69,8 @@ def test_oracle_epsilon_query_is_the_reference(name):
 
 GS = np.load(os.path.join(os.path.dirname(__file__), "golden",
                           "neighbors_sparse_ref.npz"))
-DBS = sorted({k.split("__")[0] for k in GS.files})
+DBS = sorted({k.split("__")[0] for k in GS.files if k.startswith("dbs_")})
+KNS = sorted({k.split("__")[0] for k in GS.files if k.startswith("kns_")})
 
 
 def sparse_case(name):
@@ -115,3 +116,50 @@ def test_oracle_sparse_distances_are_sklearns_expansion():
             want = sk.pairwise_distances(m[q], m).ravel()
             got = np.sqrt(orc.csr_sq_distances(ip, ix, dv, q))
             assert np.array_equal(got, want), (name, q)
+
+
+def sparse_knn_case(name):
+    """(fit csr, query csr, d, subset, n_neighbors, dist, ind) of a sparse
+    kneighbors golden; csr = (indptr, indices, data)."""
+    f = tuple(GS[name + "__f" + a] for a in ("indptr", "indices", "data"))
+    q = tuple(GS[name + "__q" + a] for a in ("indptr", "indices", "data"))
+    sub, kn, d = (int(v) for v in GS[name + "__meta"])
+    return f, q, d, sub, kn, GS[name + "__dist"], GS[name + "__ind"]
+
+
+def assert_knn_same_up_to_ties(dist, ind, rdist, rind, what):
+    """Distances bit-exact; indices equal except among exactly equal
+    distances, which the reference's argpartition / quicksort argsort order
+    arbitrarily (the whole tie group at the list's end may also be a
+    different subset of it)."""
+    assert np.array_equal(dist, rdist), what
+    if np.array_equal(ind, rind):
+        return
+    for r in np.nonzero((ind != rind).any(1))[0]:
+        for v in np.unique(dist[r]):
+            at = dist[r] == v
+            if v == dist[r, -1]:
+                continue        # the last tie group may be another subset
+            assert np.array_equal(np.sort(ind[r, at]), np.sort(rind[r, at])), \
+                (what, r)
+
+
+@pytest.mark.parametrize("name", KNS)
+def test_oracle_sparse_kneighbors_is_the_reference(name):
+    f, q, d, sub, kn, dist, ind = sparse_knn_case(name)
+    got_d, got_i = orc.kneighbors_csr(f, q, kn)
+    assert_knn_same_up_to_ties(got_d, got_i, dist, ind, name)
+    # the indices name rows at the reported distances
+    fm = sp_matrix(f, d)
+    qm = sp_matrix(q, d)
+    for r in (0, qm.shape[0] // 2, qm.shape[0] - 1):
+        want = np.sqrt(orc.csr_sq_distances_to(
+            qm[r].indices, qm[r].data, *f))
+        assert np.array_equal(want[ind[r]], dist[r]), (name, r)
+    del fm
+
+
+def sp_matrix(csr, d):
+    sp = pytest.importorskip("scipy.sparse")
+    ip, ix, dv = csr
+    return sp.csr_matrix((dv, ix, ip), shape=(ip.size - 1, d))

@@ -10,6 +10,9 @@ kneighbors: queries/s against a fit set of nfit rows (dkm_knn_f64), with
   CPU: the reference algorithm (oracle.neighbors_oracle.kneighbors: sklearn
   NearestNeighbors per (query Subset, fit Subset) pair + the sort merge) on
   a sample of query rows, one process.
+kneighbors on CSR: queries/s of dkm_knn_csr_f64 (sp-kq queries against the
+  sp-n CSR rows); CPU: the reference algorithm on CSR Subsets (sklearn brute
+  force per Subset pair + the sort merge) on a sample of query rows.
 epsilon query: queries/s of dkm_radius_count + fill (+ sort) over eps-n
   rows; CPU: the reference's per-sample _vec_matrix_euclid loop
   (oracle.neighbors_oracle.compute_neighbours) on a sample of queries.
@@ -43,6 +46,7 @@ def main():
     p.add_argument("--sp-nnz", type=int, default=10)
     p.add_argument("--sp-q", type=int, default=50_000)
     p.add_argument("--sp-eps", type=float, default=1.5)
+    p.add_argument("--sp-kq", type=int, default=20_000)
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--no-cpu", action="store_true")
     a = p.parse_args()
@@ -90,6 +94,17 @@ def main():
                           "sample": "%d query rows against %d CSR rows, the "
                                     "reference's per-sample sklearn "
                                     "pairwise_distances loop" % (m, a.sp_n)}
+        m = 500
+        sblocks = [xs[i:i + a.subset] for i in range(0, a.sp_n, a.subset)]
+        t0 = time.perf_counter()
+        orc.kneighbors(sblocks, [xs[:m]], a.kn)
+        el = time.perf_counter() - t0
+        cpu["knn_csr"] = {"value": m / el, "unit": "queries/s", "cores": 1,
+                          "kind": "port", "seconds": el,
+                          "sample": "%d CSR query rows against %d CSR rows "
+                                    "(%d Subsets), sklearn brute force per "
+                                    "Subset pair + sort merge"
+                                    % (m, a.sp_n, len(sblocks))}
 
     import torch
     from dislib_amd.cluster.dbscan import compute_neighbours
@@ -170,8 +185,34 @@ def main():
     if "eps_csr" in cpu:
         eps_csr["cpu_baseline"] = cpu["eps_csr"]
         eps_csr["gpu_over_cpu"] = eps_csr["value"] / cpu["eps_csr"]["value"]
+    sp_fit = load_data(xs, subset_size=a.subset)
+    sp_q = load_data(xs[:a.sp_kq], subset_size=a.subset)
+    nn = NearestNeighbors(n_neighbors=a.kn)
+    nn.fit(sp_fit)
+    nn.kneighbors(sp_q)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        nn.kneighbors(sp_q)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    t = min(ts)
+    pairs = float(a.sp_kq) * a.sp_n
+    knn_csr = {"workload": "kneighbors, sparse: %d queries x %d CSR rows, "
+                           "d=%d, %d nnz/row, k=%d"
+                           % (a.sp_kq, a.sp_n, a.sp_d, a.sp_nnz, a.kn),
+               "value": a.sp_kq / t, "unit": "queries/s", "seconds": t,
+               "pairs_per_s": pairs / t,
+               "includes": "host concatenation + upload of both CSR "
+                           "matrices, the partial lists, the merge and the "
+                           "copy back"}
+    if "knn_csr" in cpu:
+        knn_csr["cpu_baseline"] = cpu["knn_csr"]
+        knn_csr["gpu_over_cpu"] = knn_csr["value"] / cpu["knn_csr"]["value"]
     print(json.dumps({"kneighbors": knn, "epsilon_query": eps,
-                      "epsilon_query_csr": eps_csr}), flush=True)
+                      "epsilon_query_csr": eps_csr,
+                      "kneighbors_csr": knn_csr}), flush=True)
 
 
 if __name__ == "__main__":

@@ -19,6 +19,8 @@ PT="python -u -m pytest -p no:cacheprovider --timeout 200 --timeout-method threa
 for s in "$@"; do
   case $s in
     t_new) step t_new 600 $PT tests/test_gpu_sorted.py tests/test_gpu_b2.py tests/test_gpu_nonfinite.py tests/test_gpu_fullsize.py ;;
+    t_nb) step t_nb 600 $PT tests/test_gpu_neighbors.py ;;
+    t_c5) step t_c5 600 $PT tests/test_gpu_fullsize.py -k c5 ;;
     t_all) step t_all 900 $PT -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
