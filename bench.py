@@ -398,8 +398,8 @@ def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
                "streamed_frac": n * sb / sec / 1e9 / HBM_PEAK_GBS}
     else:
         # auto mode runs the single-product GEMM screen (bf16 hi x hi on
-        # hi-only tiles, features padded to 64)
-        dp, kp = (d + 63) // 64 * 64, (k + 255) // 256 * 256
+        # hi-only tiles, features padded to 32)
+        dp, kp = (d + 31) // 32 * 32, (k + 255) // 256 * 256
         f = 2.0 * kp * dp * n
         out = {"bound": "mfma", "achieved": f / sec / 1e12,
                "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -410,7 +410,10 @@ def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
                "kernel_ms": r["kern_ms"],
                "alg_fp64_equiv_tflops": 2.0 * k * d * n / sec / 1e12,
                "fp64_peak_tflops": FP64_PEAK_TFLOPS,
-               "hbm_gbs": n * es * d / sec / 1e9}
+               "hbm_gbs": n * es * d / sec / 1e9,
+               "image": ("bf16 GEMM tiles (resident, built in the fit)"
+                         if r.get("image_kind", 0) == 4 else
+                         "none (X split per chunk on a second stream)")}
     out["traffic"] = None
     out["binding"] = binding_for(d, k, csr_nnz)
     return out

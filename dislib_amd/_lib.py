@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("DKM_LIB", os.path.join(_HERE, "libdkm.so"))
 ABI_VERSION = 2
 MODE_AUTO, MODE_EXACT, MODE_SCREEN32, MODE_BF16X3, MODE_BF16 = 0, 1, 2, 3, 4
 MODE_MASK, MODE_NOHINT, MODE_B1 = 0xff, 0x100, 0x200
-IMAGE_NONE, IMAGE_SINGLE, IMAGE_SPLIT, IMAGE_SORTED = 0, 1, 2, 3
+IMAGE_NONE, IMAGE_SINGLE, IMAGE_SPLIT, IMAGE_SORTED, IMAGE_GEMM = 0, 1, 2, 3, 4
 SUMS_F64, SUMS_F32, SUMS_RECIP = 0, 1, 2
 PREP_CSR = 1
 COMM_ID_BYTES = 128

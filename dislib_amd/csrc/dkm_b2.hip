@@ -1011,6 +1011,10 @@ static int64_t img_tile_bytes(int64_t d, int kind) {
 }
 
 size_t x_image_bytes(int64_t n, int64_t d, int kind) {
+  if (kind == IMG_GEMM) {
+    const int64_t ntg = (n + GT - 1) / GT;
+    return (size_t)ntg * (dpad32(d) / GBK) * GSTAGE1 + (size_t)ntg * GT * 4;
+  }
   const int64_t nt = (n + 31) / 32;
   return (size_t)nt * img_tile_bytes(d, kind) + (size_t)nt * 128 +
          (kind == IMG_SORTED ? (size_t)nt * 256 : 0);
@@ -1019,6 +1023,16 @@ size_t x_image_bytes(int64_t n, int64_t d, int kind) {
 XImage x_image_view(const void *image, int64_t n, int64_t d, int kind) {
   const int64_t nt = (n + 31) / 32;
   XImage im;
+  if (kind == IMG_GEMM) {
+    const int64_t ntg = (n + GT - 1) / GT;
+    im.tiles = (const uint16_t *)image;
+    im.xx = (const float *)((const char *)image +
+                            (size_t)ntg * (dpad32(d) / GBK) * GSTAGE1);
+    im.kind = kind;
+    im.perm = nullptr;
+    im.plab = nullptr;
+    return im;
+  }
   im.tiles = (const uint16_t *)image;
   im.xx = (const float *)((const char *)image +
                           (size_t)nt * img_tile_bytes(d, kind));

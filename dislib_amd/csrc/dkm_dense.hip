@@ -2883,7 +2883,7 @@ template <class TX>
 static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
                        const double *C, int k, const WsView &v, size_t wsb,
                        int32_t *labels, double *acc, int acc_kind,
-                       bool one, hipStream_t s) {
+                       bool one, const XImage *img, hipStream_t s) {
   (void)wsb;
   const int64_t nq = std::min<int64_t>(v.nq, INT32_MAX);
   if (!labels && nq < 1)
@@ -2903,7 +2903,7 @@ static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
     const int64_t end = std::min(n, base + chunk);
     int32_t *lab_out = labels ? labels : v.queue - base;
     int r = gemm_screen<TX>(X, base, end, d, ldx, C, k, v, lab_out,
-                            skind ? acc : nullptr, skind == 2, one, s);
+                            skind ? acc : nullptr, skind == 2, one, img, s);
     if (r) return r;
     if (post && (r = launch_post_sums<TX>(X, base, end, d, ldx, lab_out,
                                           prevbuf, k, acc, v, s)))
@@ -2939,6 +2939,10 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                    (screen_ok(k, d) && b1_ok(k, d) && !sums_fit_lds(k, d))
                ? DKM_MODE_SCREEN_BF16
                : DKM_MODE_SCREEN_BF16X3;
+  if (image && (image_kind < IMG_SINGLE || image_kind > IMG_GEMM ||
+                (image_kind == IMG_GEMM) != gemm_path(k, d)))
+    return fail(DKM_E_ARG, std::string(who) +
+                               ": image kind does not fit (k, d)");
   // the sorted image keeps a copy of the labels that only k_screen_b2
   // maintains: any other arithmetic would leave it stale
   if (image && image_kind == IMG_SORTED &&
@@ -2953,8 +2957,14 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
       gemm_path(k, d)) {
     WsView v;
     if (int r = ws_view(ws, wsb, k, d, &v)) return r;
+    // the resident sample tiles serve the single-product screen only
+    XImage gimg;
+    const bool use_img = image && image_kind == IMG_GEMM &&
+                         mode == DKM_MODE_SCREEN_BF16;
+    if (use_img) gimg = x_image_view(image, n, d, IMG_GEMM);
     return launch_gemm<TX>(X, n, (int)d, ldx, C, (int)k, v, wsb, labels, acc,
-                           acc_kind, mode == DKM_MODE_SCREEN_BF16, s);
+                           acc_kind, mode == DKM_MODE_SCREEN_BF16,
+                           use_img ? &gimg : nullptr, s);
   }
   if (mode == DKM_MODE_SCREEN32 || mode == DKM_MODE_SCREEN_BF16X3 ||
       mode == DKM_MODE_SCREEN_BF16) {
@@ -2979,15 +2989,21 @@ template <class TX>
 static int x_image(const TX *X, int64_t n, int64_t d, int64_t ldx, int kind,
                    void *image, size_t image_bytes, void *stream,
                    const char *who) {
-  if (n < 0 || d <= 0 || ldx < d)
+  if (n < 0 || d <= 0 || ldx < d || d > INT32_MAX)
     return fail(DKM_E_ARG, std::string(who) + ": bad n/d/ldx");
-  if (d > 128) return fail(DKM_E_ARG, std::string(who) + ": d > 128");
+  if (kind == IMG_GEMM ? d <= 128 : d > 128)
+    return fail(DKM_E_ARG, std::string(who) +
+                               ": the GEMM image needs d > 128, the others "
+                               "d <= 128");
   if (n == 0) return 0;
   if (!X || !image) return fail(DKM_E_ARG, std::string(who) + ": NULL");
-  if (kind != IMG_SINGLE && kind != IMG_SPLIT)
+  if (kind != IMG_SINGLE && kind != IMG_SPLIT && kind != IMG_GEMM)
     return fail(DKM_E_ARG, std::string(who) + ": bad image kind");
   if (image_bytes < x_image_bytes(n, d, kind))
     return fail(DKM_E_WORKSPACE, std::string(who) + ": image too small");
+  if (kind == IMG_GEMM)
+    return gemm_image<TX>(X, n, (int)d, ldx, x_image_view(image, n, d, kind),
+                          (hipStream_t)stream);
   return launch_x_image<TX>(X, n, (int)d, ldx, kind, image, dev_info().cus,
                             (hipStream_t)stream);
 }
@@ -3090,9 +3106,12 @@ int dkm_predict_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
 }
 
 int dkm_x_image_kind(int64_t k, int64_t d, int mode) {
-  if (k <= 0 || d <= 0 || d > 128 || k > INT32_MAX) return IMG_NONE;
-  if (gemm_path(k, d) || !screen_ok(k, d)) return IMG_NONE;
+  if (k <= 0 || d <= 0 || k > INT32_MAX || d > INT32_MAX) return IMG_NONE;
   mode &= DKM_MODE_MASK;
+  if (gemm_path(k, d))  // AUTO picks the single-product GEMM screen
+    return mode == DKM_MODE_AUTO || mode == DKM_MODE_SCREEN_BF16 ? IMG_GEMM
+                                                                 : IMG_NONE;
+  if (d > 128 || !screen_ok(k, d)) return IMG_NONE;
   if (mode == DKM_MODE_AUTO)
     mode = b1_ok(k, d) && !sums_fit_lds(k, d) ? DKM_MODE_SCREEN_BF16
                                               : DKM_MODE_SCREEN_BF16X3;
@@ -3109,7 +3128,9 @@ int dkm_x_image_kind(int64_t k, int64_t d, int mode) {
 }
 
 size_t dkm_x_image_bytes(int64_t n, int64_t d, int kind) {
-  if (n < 0 || d <= 0 || d > 128) return 0;
+  if (n < 0 || d <= 0 || d > INT32_MAX) return 0;
+  if (kind == IMG_GEMM) return d > 128 ? x_image_bytes(n, d, kind) : 0;
+  if (d > 128) return 0;
   if (kind == IMG_SPLIT && d > 32) return 0;
   if (kind != IMG_SINGLE && kind != IMG_SPLIT && kind != IMG_SORTED) return 0;
   return x_image_bytes(n, d, kind);

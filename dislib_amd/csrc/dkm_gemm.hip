@@ -17,8 +17,9 @@
 //   k_gemm_merge   per sample: the smallest scores over all centre tiles, a
 //                  rigorous error bound 2B, and the decision: one score
 //                  within 2B of the best -> label; a few -> the reference
-//                  arithmetic on exactly those candidates; more than the
-//                  tiles kept -> left for k_recheck_exact (labels[i] < 0).
+//                  arithmetic on exactly those candidates (k_gemm_cand);
+//                  more within 2B in a tile than it kept -> k_gemm_full,
+//                  which scans those tiles whole.
 //
 // Tile layout (centres and samples alike): tile t, stage ks = 256 rows x
 // 128 B; a row holds features 32ks..32ks+31 as bf16 hi (chunks 0-3) and lo
@@ -67,6 +68,10 @@ constexpr int64_t GLIST2 = (int64_t)TL_SEGS * TL_CAP / 2;
 __host__ __device__ __forceinline__ int gslot(int row, int c) {
   return c ^ ((row >> 1) & 7);
 }
+// hi-only 64-B rows (4 chunks): chunk c of row r at slot c ^ ((r >> 2) & 3)
+__host__ __device__ __forceinline__ int gslot1(int row, int c) {
+  return c ^ ((row >> 2) & 3);
+}
 
 // v_med3 against an opaque -inf: a min without fminf's NaN canonicalisation
 __device__ __forceinline__ float g_opaque_ninf() {
@@ -78,7 +83,7 @@ __device__ __forceinline__ float g_opaque_ninf() {
 // (value, centre) lexicographic insertion into an ascending top-4 list,
 // branchless (c0 => c1 => c2 => c3 on a sorted list; no runtime indices)
 __device__ __forceinline__ bool vi_less(float a, int ia, float b, int ib) {
-  return a < b || (a == b && ia < ib);
+  return (a < b) | ((a == b) & (ia < ib));  // bitwise: no branches
 }
 __device__ __forceinline__ void top_insert(float v, int i, float (&V)[GTOP],
                                            int (&I)[GTOP]) {
@@ -110,9 +115,8 @@ __global__ void __launch_bounds__(256)
   const int lane = threadIdx.x & 63, rr = lane >> 3, f = lane & 7;
   const int64_t wv = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nw = (int64_t)gridDim.x * 4;
-  // 8-feature groups: 4 per 32-feature hi/lo stage, 8 per 64-feature
-  // hi-only stage (one)
-  const int ngrp = nks * (one ? 8 : 4);
+  // 8-feature groups: 4 per 32-feature stage (hi/lo, or hi only: one)
+  const int ngrp = nks * 4;
   for (int64_t rb = wv * 8; rb < mrows; rb += nw * 8) {
     const int64_t row = rb + rr;
     const bool valid = row < nrows;
@@ -166,9 +170,9 @@ __global__ void __launch_bounds__(256)
         lw[q] = __builtin_bit_cast(uint32_t, l2);
       }
       if (one) {
-        const int ks = g >> 3, c = g & 7;
-        char *tile = out + (st * nks + ks) * (int64_t)GSTAGE + r * 128;
-        *(uint4 *)(tile + 16 * gslot(r, c)) =
+        const int ks = g >> 2, c = g & 3;
+        char *tile = out + (st * nks + ks) * (int64_t)GSTAGE1 + r * 64;
+        *(uint4 *)(tile + 16 * gslot1(r, c)) =
             make_uint4(hw[0], hw[1], hw[2], hw[3]);
       } else {
         const int ks = g >> 2, c = g & 3;
@@ -195,15 +199,14 @@ __global__ void k_gemm_cnorm(const float *__restrict__ cn32, int64_t k,
 }
 
 // ---------------------------------------------------------------------------
-// screen: one workgroup = centre tile ct x sample tile st, full K.
+// bf16x3 screen: one workgroup = centre tile ct x sample tile st, full K.
 // Wave w: wm = w & 1 -> centres wm*128 .. +127 (4 blocks of 32 = A rows),
 // wn = w >> 1 -> samples wn*64 .. +63 (2 blocks of 32 = B columns).
 // 32x32x16 accumulator register g of lane (r, h): centre row
 // (g & 3) + 8 (g >> 2) + 4h of the block, sample column r.
 // ---------------------------------------------------------------------------
-template <int NP>  // MFMA products per term: 3 (bf16x3) or 1 (hi x hi)
 __global__ void __launch_bounds__(GTHREADS)
-    k_gemm_screen(const char *__restrict__ afrag, const float *__restrict__ gcn,
+    k_gemm_screen3(const char *__restrict__ afrag, const float *__restrict__ gcn,
                   const char *__restrict__ xs, int nst, int nct, int nks,
                   int2 *__restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -279,22 +282,21 @@ __global__ void __launch_bounds__(GTHREADS)
     const char *la = lds + buf * (2 * GSTAGE);
     const char *lb = la + GSTAGE;
 #pragma unroll
-    for (int s = 0; s < (NP == 1 ? 4 : 2); ++s) {
-      // hi-only rows (NP == 1): K-substep s reads hi chunk 2s + h
-      const int oh = NP == 1 ? 16 * ((2 * s + h) ^ sw) : (s ? oh1 : oh0);
+    for (int s = 0; s < 2; ++s) {
+      const int oh = s ? oh1 : oh0;
       const int ol = s ? ol1 : ol0;
       bf16x8 ah[4], al[4], bh[2], bl[2];
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) {
         const char *p = la + arow + mb * 32 * 128;
         ah[mb] = *(const bf16x8 *)(p + oh);
-        if constexpr (NP == 3) al[mb] = *(const bf16x8 *)(p + ol);
+        al[mb] = *(const bf16x8 *)(p + ol);
       }
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         const char *p = lb + brow + nb * 32 * 128;
         bh[nb] = *(const bf16x8 *)(p + oh);
-        if constexpr (NP == 3) bl[nb] = *(const bf16x8 *)(p + ol);
+        bl[nb] = *(const bf16x8 *)(p + ol);
       }
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb)
@@ -302,20 +304,18 @@ __global__ void __launch_bounds__(GTHREADS)
         for (int nb = 0; nb < 2; ++nb)
           acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
               ah[mb], bh[nb], acc[mb][nb], 0, 0, 0);
-      if constexpr (NP == 3) {
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
+      for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-          for (int nb = 0; nb < 2; ++nb)
-            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                ah[mb], bl[nb], acc[mb][nb], 0, 0, 0);
+        for (int nb = 0; nb < 2; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              ah[mb], bl[nb], acc[mb][nb], 0, 0, 0);
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb)
+      for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-          for (int nb = 0; nb < 2; ++nb)
-            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                al[mb], bh[nb], acc[mb][nb], 0, 0, 0);
-      }
+        for (int nb = 0; nb < 2; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              al[mb], bh[nb], acc[mb][nb], 0, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // buffer `buf` is free for stage ks + 2
@@ -369,6 +369,241 @@ __global__ void __launch_bounds__(GTHREADS)
     int2 *out = part + ((int64_t)(st * GT + tid) * nct + ct) * GTOP;
 #pragma unroll
     for (int e = 0; e < GTOP; ++e) out[e] = make_int2(__float_as_int(V[e]), I[e]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// single-product screen (hi x hi), persistent: one 512-thread workgroup per
+// CU walks its share of the (sample tile, centre tile) pairs as one stream
+// of 32-feature stages, so the loads of the next tile's first stages fly
+// while the current tile finishes and its epilogue runs.
+//   * XCD-aware split: workgroup b runs on XCD b & 7; XCD x owns a
+//     contiguous range of the pairs (centre tile fastest) and its workgroups
+//     take them round-robin, so at any time one XCD's CUs work on a few
+//     sample tiles against all centre tiles (the sample tile is read from
+//     HBM once, then from that XCD's L2).
+//   * a 4-stage LDS ring (4 x 32 KB), 3 stages in flight, ONE barrier per
+//     stage: the barrier of stage q also proves every wave is done with
+//     stage q - 1, whose buffer (q + 3) & 3 then takes stage q + 3.
+//   * global_load_lds (asm: see glds16) with the stage base in SGPRs and
+//     the per-lane offset a constant VGPR (no address arithmetic per load).
+//   * rows of 64 B (32 features) with 16-B chunk c at c ^ ((row >> 2) & 3):
+//     every 16-lane group of a ds_read_b128 hits 16 distinct slots.
+//   * epilogue: each lane keeps the GTOP smallest packed scores of its 64
+//     (a med3 chain, the tag by one and-or), written to LDS as bare floats,
+//     sample-minor (conflict-free; the tag names the centre), then thread =
+//     sample merges the 4 sources into the tile's sorted top-GTOP.  (Keeping
+//     only 2 or 3 per lane is cheaper but sends every sample with that many
+//     candidates in one source to the full scan: measured slower per fit.)
+// Wave w: wm = w & 1 -> centres wm*128 .. +127, wn = w >> 1 -> samples
+// wn*64 .. +63, accumulator layout as k_gemm_screen3.
+// ---------------------------------------------------------------------------
+constexpr int G1RING = 4;
+
+// 16 B per lane from gbase + voff (gbase wave-uniform) into LDS at
+// lds_addr + 16 lane (wave-uniform; M0 written in the same statement).  An
+// asm statement, so hipcc adds no vmcnt wait of its own before LDS accesses
+// it cannot prove disjoint (it would drain the ring on every stage): the
+// kernel counts these copies itself.
+__device__ __forceinline__ void glds16(const char *gbase, uint32_t voff,
+                                       uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(gbase), "s"(lds_addr)
+      : "memory");
+}
+constexpr int G1STAGE = 2 * GSTAGE1;             // A + B bytes of one stage
+constexpr int G1MRG = G1RING * G1STAGE;    // epilogue [GTOP][4][GT] floats
+constexpr int G1NRM = G1MRG + 4 * 4 * GT * 4;  // |c|^2 of 2 tiles
+constexpr int G1LDS = G1NRM + 2 * GT * 4;
+
+__global__ void __launch_bounds__(GTHREADS)
+    k_gemm_screen1(const char *__restrict__ afrag,
+                   const float *__restrict__ gcn, const char *__restrict__ xs,
+                   int nst, int nct, int nks, int2 *__restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  typedef __attribute__((address_space(3))) void lds_void;
+  const int G = nst * nct;
+  const int per = (int)(gridDim.x >> 3);  // workgroups per XCD
+  const int xcd = (int)(blockIdx.x & 7), j = (int)(blockIdx.x >> 3);
+  const int q8 = G >> 3, r8 = G & 7;
+  const int lo = xcd * q8 + (xcd < r8 ? xcd : r8);
+  const int cnt = q8 + (xcd < r8 ? 1 : 0);
+  const int ntile = j < cnt ? (cnt - j + per - 1) / per : 0;
+  if (ntile == 0) return;  // workgroup-uniform
+  const int Q = ntile * nks;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5, wm = w & 1, wn = w >> 1;
+  const uint32_t voff = (uint32_t)(w * 1024 + lane * 16), voff2 = voff + 8192;
+  const uint32_t voffn = (uint32_t)(lane * 16);
+  // this wave's 1-KB piece of each 8-KB half of an operand stage
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_void *)lds;
+  const uint32_t lds_base =
+      __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)w * 1024u);
+  const uint32_t nrm_base =
+      __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(G1NRM + w * 128));
+  const int64_t tbytes = (int64_t)nks * GSTAGE1;  // one tile, every stage
+
+  auto issue = [&](int q) {  // stage q -> ring buffer q & 3
+    const int m = q / nks, ks = q - m * nks;
+    const int t = lo + j + m * per;
+    const int st = t / nct, ct = t - st * nct;
+    const char *ga = afrag + ct * tbytes + (int64_t)ks * GSTAGE1;
+    const char *gb = xs + st * tbytes + (int64_t)ks * GSTAGE1;
+    const uint32_t la = lds_base + (uint32_t)((q & (G1RING - 1)) * G1STAGE);
+    glds16(ga, voff, la);
+    glds16(ga, voff2, la + 8192);
+    glds16(gb, voff, la + GSTAGE1);
+    glds16(gb, voff2, la + GSTAGE1 + 8192);
+    if (ks == 0 && lane < 8)  // the tile's 256 |c|^2: 128 B per wave
+      glds16((const char *)(gcn + (int64_t)ct * GT + w * 32), voffn,
+             nrm_base + (uint32_t)((m & 1) * GT * 4));
+  };
+
+  // accumulators start from |c|^2 of their centre rows (LDS: copied with
+  // the tile's first stage, so no global load waits behind the ring)
+  f32x16 acc[4][2];
+  auto init_acc = [&](int m) {
+    const float *nl = (const float *)(lds + G1NRM) + (m & 1) * GT;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      const float *cp = nl + wm * 128 + mb * 32 + 4 * h;
+      f32x16 init;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const f32x4 c4 = *(const f32x4 *)(cp + 8 * qq);
+        init[4 * qq + 0] = c4.x;
+        init[4 * qq + 1] = c4.y;
+        init[4 * qq + 2] = c4.z;
+        init[4 * qq + 3] = c4.w;
+      }
+      acc[mb][0] = init;
+      acc[mb][1] = init;
+    }
+  };
+
+  const float ninf = g_opaque_ninf();
+  float *mrg = (float *)(lds + G1MRG);  // [GTOP e][4 src][GT samples]
+  auto epilogue = [&](int st, int ct) {
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      float v[GTOP];
+#pragma unroll
+      for (int e = 0; e < GTOP; ++e) v[e] = INFINITY;
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const float p = __uint_as_float(
+              (__float_as_uint(acc[mb][nb][g]) & ~GTAG) |
+              (uint32_t)(mb * 16 + g));
+#pragma unroll
+          for (int e = GTOP - 1; e > 0; --e)
+            v[e] = __builtin_amdgcn_fmed3f(v[e - 1], v[e], p);
+          v[0] = __builtin_amdgcn_fmed3f(v[0], p, ninf);
+        }
+      const int sample = wn * 64 + nb * 32 + r, src = wm * 2 + h;
+#pragma unroll
+      for (int e = 0; e < GTOP; ++e) mrg[(e * 4 + src) * GT + sample] = v[e];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (tid < GT) {
+      float V[GTOP];
+      int I[GTOP];
+#pragma unroll
+      for (int e = 0; e < GTOP; ++e) {
+        V[e] = INFINITY;
+        I[e] = 0x7fffffff;
+      }
+#pragma unroll
+      for (int e = 0; e < GTOP; ++e)
+#pragma unroll
+        for (int src = 0; src < 4; ++src) {
+          const float qv = mrg[(e * 4 + src) * GT + tid];
+          // the centre from the tag: source (wm', h') = (src >> 1, src & 1)
+          const uint32_t tg = __float_as_uint(qv) & GTAG;
+          const int mb = (int)(tg >> 4), g = (int)(tg & 15);
+          const int qi = ct * GT + (src >> 1) * 128 + mb * 32 + (g & 3) +
+                         8 * (g >> 2) + 4 * (src & 1);
+          top_insert(qv, qi, V, I);
+        }
+      int2 *out = part + ((int64_t)(st * GT + tid) * nct + ct) * GTOP;
+#pragma unroll
+      for (int e = 0; e < GTOP; ++e)
+        out[e] = make_int2(__float_as_int(V[e]), I[e]);
+    }
+  };
+
+  // lane's chunk offsets in a 64-B row: K-substep s reads features
+  // 16s + 8h .. +7, chunk 2s + h
+  const int sw = (r >> 2) & 3;
+  const int o0 = 16 * ((0 + h) ^ sw), o1 = 16 * ((2 + h) ^ sw);
+  const int arow = (wm * 128 + r) * 64, brow = (wn * 64 + r) * 64;
+
+  // stage q: its copies landed (this wave: later stages may stay in
+  // flight; every wave: the barrier), this wave's LDS reads of stage q - 1
+  // done (its buffer takes stage q + 3 after the barrier)
+  auto sync_issue = [&](int q) {
+    const int ahead = Q - 1 - q;
+    if (ahead >= 2)
+      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    else if (ahead == 1)
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (q + 3 < Q) issue(q + 3);
+  };
+  // K-substep s of stage q into registers.  Per stage, after its barrier:
+  // read substep 0, MFMAs of the previous stage's substep 1, read substep 1,
+  // MFMAs of substep 0 -- every LDS read hides under 8 MFMAs.
+  auto load_sub = [&](int q, int s, bf16x8 (&A)[4], bf16x8 (&B)[2]) {
+    const char *la = lds + (q & (G1RING - 1)) * G1STAGE;
+    const char *lb = la + GSTAGE1;
+    const int oh = s ? o1 : o0;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+      A[mb] = *(const bf16x8 *)(la + arow + mb * 32 * 64 + oh);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+      B[nb] = *(const bf16x8 *)(lb + brow + nb * 32 * 64 + oh);
+  };
+  auto mfmas = [&](const bf16x8 (&A)[4], const bf16x8 (&B)[2]) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+        acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            A[mb], B[nb], acc[mb][nb], 0, 0, 0);
+  };
+
+  for (int q = 0; q < 3 && q < Q; ++q) issue(q);
+  bf16x8 A0[4], A1[4], B0[2], B1[2];
+  for (int m = 0; m < ntile; ++m) {  // workgroup-uniform
+    const int t = lo + j + m * per;
+    const int st = t / nct, ct = t - st * nct;
+    const int q0 = m * nks;
+    sync_issue(q0);
+    init_acc(m);
+    load_sub(q0, 0, A0, B0);
+    load_sub(q0, 1, A1, B1);
+    mfmas(A0, B0);
+    for (int ks = 1; ks < nks; ++ks) {
+      sync_issue(q0 + ks);
+      load_sub(q0 + ks, 0, A0, B0);
+      mfmas(A1, B1);
+      load_sub(q0 + ks, 1, A1, B1);
+      mfmas(A0, B0);
+    }
+    mfmas(A1, B1);
+    epilogue(st, ct);
   }
 }
 
@@ -547,7 +782,7 @@ __global__ void __launch_bounds__(256)
                  int64_t ldx, int k, int nct, int dpad,
                  const int2 *__restrict__ part, const float *__restrict__ xnv,
                  WsView v, int32_t *__restrict__ lab_out, double *acc,
-                 int flags) {
+                 int flags, int64_t lofs) {
   const float cm =
       (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
   const int lane = threadIdx.x & 63;
@@ -578,9 +813,10 @@ __global__ void __launch_bounds__(256)
         slot = atomicAdd(L ? &v.hdr->gcount2 : &v.hdr->gcount,
                          (uint32_t)__popcll(m));
       slot = __shfl(slot, 0, 64);
+      // the overflow list spans the call (deferred): rows from its base
       if (list == L)
         v.tlist[(L ? GLIST2 : 0) + slot + __popcll(m & ((1ull << lane) - 1))] =
-            make_int2((int)i, prev);
+            make_int2((int)(L ? lofs + i : i), prev);
     }
   }
 }
@@ -673,10 +909,14 @@ __global__ void __launch_bounds__(256)
 }
 
 // ---------------------------------------------------------------------------
-// full scan: one 1024-thread workgroup per listed sample whose kept scores
-// cannot bound the candidates (or whose bound does not hold: NaN, overflow):
-// the reference arithmetic on every centre (C^T reads, coalesced over the
-// lanes' centres), then the workgroup's first-index argmin.
+// overflow scan: the samples whose kept scores cannot bound the candidates
+// (some centre tile holds more than GTOP scores within the limit; or the
+// bound does not hold: NaN, overflow), deferred over the chunks of a call
+// (a few hundred per 10M rows on the first iterations, none later) and
+// scanned here in one launch: one 1024-thread workgroup per sample, every
+// centre by the reference arithmetic (lanes over centres: coalesced C^T
+// reads), then the workgroup's argmin in np.argmin's order (first NaN, else
+// the smallest value, then index).
 // ---------------------------------------------------------------------------
 template <class TX>
 __global__ void __launch_bounds__(1024)
@@ -687,9 +927,13 @@ __global__ void __launch_bounds__(1024)
   __shared__ int bi[16];
   const uint32_t cnt = v.hdr->gcount2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && cnt)  // diagnostics
+  if (blockIdx.x == 0 && threadIdx.x == 0 && cnt) {  // diagnostics
     atomicAdd((unsigned long long *)&v.hdr->rechecked_total,
               (unsigned long long)cnt);
+    atomicAdd((unsigned long long *)&v.hdr->reserved[4],
+              (unsigned long long)cnt);
+  }
+  const int64_t ldc = ct_ld(k);
   for (uint32_t e = blockIdx.x; e < cnt; e += gridDim.x) {
     const int2 it = v.tlist[GLIST2 + e];
     const int64_t si = row0 + it.x;
@@ -698,7 +942,7 @@ __global__ void __launch_bounds__(1024)
     int lab = 0x7fffffff;  // lanes without a centre never win
     for (int jc = threadIdx.x; jc < k; jc += 1024) {
       const double dist =
-          sqrt(pw_sum(SqDiffT<TX>{xr, v.ct64 + jc, ct_ld(k)}, d));
+          sqrt(pw_sum(SqDiffT<TX>{xr, v.ct64 + jc, ldc}, d));
       if (nan_first_less(dist, jc, best, lab)) {
         best = dist;
         lab = jc;
@@ -739,7 +983,7 @@ template <class TX>
 int launch_split(const TX *X, int64_t row0, int64_t nrows, int64_t mrows,
                  int d, int64_t ldx, double scale, char *out, float *xn,
                  int one, hipStream_t s) {
-  const int nks = one ? (int)(dpad64(d) / 64) : (int)(dpad32(d) / GBK);
+  const int nks = (int)(dpad32(d) / GBK);
   const bool vec = (d % 8 == 0) && ((ldx * (int64_t)sizeof(TX)) % 16 == 0) &&
                    ((uintptr_t)X % 16 == 0);
   const int64_t blocks = std::min<int64_t>((mrows + 31) / 32, 16384);
@@ -773,6 +1017,7 @@ int gemm_prepare(const double *C, int64_t k, int64_t d, const WsView &v,
 // host thread (created at first use, kept for the process)
 struct SplitStream {
   hipStream_t s = nullptr;
+  int cus = 256;  // compute units of the device
   hipEvent_t split_ev[2] = {nullptr, nullptr}, free_ev[2] = {nullptr, nullptr};
   bool ok = false;
 };
@@ -789,6 +1034,11 @@ static SplitStream &split_stream() {
                                      hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&x.free_ev[i],
                                      hipEventDisableTiming) == hipSuccess;
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount,
+                              dev) == hipSuccess &&
+        cu >= 8)
+      x.cus = cu;
     x.ok = good;
   }
   return x;
@@ -797,19 +1047,22 @@ static SplitStream &split_stream() {
 template <class TX>
 int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
                 const double *C, int k, const WsView &v, int32_t *lab_out,
-                double *acc, bool delta, bool one, hipStream_t s) {
+                double *acc, bool delta, bool one, const XImage *img,
+                hipStream_t s) {
   if (!v.gfrag) return fail(DKM_E_WORKSPACE, "gemm_screen: no GEMM region");
-  const void *kf = one ? (const void *)k_gemm_screen<1>
-                       : (const void *)k_gemm_screen<3>;
+  const void *kf = one ? (const void *)k_gemm_screen1
+                       : (const void *)k_gemm_screen3;
   if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          GLDS) != hipSuccess)
+                          one ? G1LDS : GLDS) != hipSuccess)
     return fail(DKM_E_LAUNCH, "gemm_screen: LDS attribute");
-  // single product: hi-only tiles, 64 features per stage
-  const int nks = one ? (int)(dpad64(d) / 64) : (int)(dpad32(d) / GBK);
+  const int nks = (int)(dpad32(d) / GBK);
   const int nct = (int)(kpad256(k) / GT);
-  const int dpad = one ? (int)dpad64(d) : (int)dpad32(d);
+  const int dpad = (int)dpad32(d);
   // bit 2: the single-product bound in the merge and candidate steps
   const int flags = (acc ? 1 : 0) | (delta ? 2 : 0) | (one ? 4 : 0);
+  // a chunk on a whole sample tile reads the resident image instead
+  const bool have_img = img && img->kind == IMG_GEMM && one;
+  auto from_img = [&](int64_t c0) { return have_img && c0 % GT == 0; };
   // The split of chunk c + 1 (HBM-bound) runs on a second stream while
   // chunk c is screened (MFMA-bound): split buffers alternate, chunk c's
   // screen waits for its split, and split c + 2 waits until chunk c's
@@ -824,6 +1077,7 @@ int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
       hipEventRecord(ss.free_ev[1], s) != hipSuccess)
     return fail(DKM_E_LAUNCH, "gemm: event");
   auto split = [&](int64_t c0, int b) -> int {
+    if (from_img(c0)) return 0;
     const int64_t rows = std::min<int64_t>(v.gchunk, end - c0);
     if (hipStreamWaitEvent(ss.s, ss.free_ev[b], 0) != hipSuccess)
       return fail(DKM_E_LAUNCH, "gemm: stream wait");
@@ -834,8 +1088,14 @@ int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
       return fail(DKM_E_LAUNCH, "gemm: event");
     return 0;
   };
-  if (base < end)
+  if (end - base > INT32_MAX)
+    return fail(DKM_E_ARG, "gemm_screen: more than 2^31 - 1 rows per call");
+  if (base < end) {
     if (int r = split(base, 0)) return r;
+    if (hipMemsetAsync(&v.hdr->gcount2, 0, 4, s) != hipSuccess)
+      return fail(DKM_E_LAUNCH, "gemm: list reset");
+  }
+  int64_t pending = 0;  // rows merged since the overflow list was scanned
   int b = 0;
   for (int64_t c0 = base; c0 < end; c0 += v.gchunk, b ^= 1) {
     const int64_t rows = std::min<int64_t>(v.gchunk, end - c0);
@@ -843,51 +1103,84 @@ int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
     const int nst = (int)(mrows / GT);
     if (c0 + v.gchunk < end)
       if (int r = split(c0 + v.gchunk, b ^ 1)) return r;
-    if (hipStreamWaitEvent(s, ss.split_ev[b], 0) != hipSuccess)
+    const char *xs = xs_b[b];
+    const float *xn = xn_b[b];
+    if (from_img(c0)) {
+      xs = (const char *)img->tiles + (c0 / GT) * (int64_t)nks * GSTAGE1;
+      xn = img->xx + c0;
+    } else if (hipStreamWaitEvent(s, ss.split_ev[b], 0) != hipSuccess) {
       return fail(DKM_E_LAUNCH, "gemm: stream wait");
+    }
     WsView vb = v;  // the merge and candidate steps read this chunk's xn
-    vb.gxn = xn_b[b];
-    if (one)
-      k_gemm_screen<1><<<(unsigned)(nst * nct), GTHREADS, GLDS, s>>>(
-          v.gfrag1, v.gcn, xs_b[b], nst, nct, nks, v.gpart);
-    else
-      k_gemm_screen<3><<<(unsigned)(nst * nct), GTHREADS, GLDS, s>>>(
-          v.gfrag, v.gcn, xs_b[b], nst, nct, nks, v.gpart);
+    vb.gxn = (float *)xn;
+    if (one) {
+      // persistent: one workgroup per CU (G1LDS of LDS each), a multiple
+      // of the 8 XCDs
+      const int64_t G = (int64_t)nst * nct;
+      const int64_t nwg = 8 * std::min<int64_t>(ss.cus / 8, (G + 7) / 8);
+      k_gemm_screen1<<<(unsigned)nwg, GTHREADS, G1LDS, s>>>(
+          v.gfrag1, v.gcn, xs, nst, nct, nks, v.gpart);
+    } else {
+      k_gemm_screen3<<<(unsigned)(nst * nct), GTHREADS, GLDS, s>>>(
+          v.gfrag, v.gcn, xs, nst, nct, nks, v.gpart);
+    }
     if (int r = check_launch("gemm screen")) return r;
-    // both list counters (gcount, gcount2: adjacent words)
-    if (hipMemsetAsync(&v.hdr->gcount, 0, 8, s) != hipSuccess)
+    if (hipMemsetAsync(&v.hdr->gcount, 0, 4, s) != hipSuccess)
       return fail(DKM_E_LAUNCH, "gemm: list reset");
     const unsigned mb = (unsigned)std::min<int64_t>((rows + 255) / 256, 8192);
     k_gemm_merge<TX><<<mb, 256, 0, s>>>(X, c0, rows, d, ldx, k, nct, dpad,
-                                        v.gpart, xn_b[b], vb, lab_out, acc,
-                                        flags);
+                                        v.gpart, xn, vb, lab_out, acc, flags,
+                                        c0 - base);
     if (int r = check_launch("gemm merge")) return r;
-    // a wave per listed sample: rows / 64 waves cover any list length
-    const unsigned cb = (unsigned)((rows + 255) / 256);
+    // a wave per listed sample, up to 8 workgroups of 4 waves per CU (the
+    // list length is known on the device only; idle waves exit at once)
+    const unsigned cb = (unsigned)std::min<int64_t>((rows + 3) / 4,
+                                                    (int64_t)ss.cus * 8);
     if (d <= 8192)
       k_gemm_cand<true, TX><<<cb, 256, 0, s>>>(X, c0, d, ldx, C, k, nct, dpad,
-                                               v.gpart, xn_b[b], vb, lab_out,
-                                               acc, flags);
+                                               v.gpart, xn, vb, lab_out, acc,
+                                               flags);
     else
       k_gemm_cand<false, TX><<<cb, 256, 0, s>>>(X, c0, d, ldx, C, k, nct,
-                                                dpad, v.gpart, xn_b[b], vb,
+                                                dpad, v.gpart, xn, vb,
                                                 lab_out, acc, flags);
     if (int r = check_launch("gemm candidates")) return r;
     if (hipEventRecord(ss.free_ev[b], s) != hipSuccess)
       return fail(DKM_E_LAUNCH, "gemm: event");
-    k_gemm_full<TX><<<256, 1024, 0, s>>>(X, c0, d, ldx, k, vb, lab_out, acc,
-                                         flags);
-    if (int r = check_launch("gemm full scan")) return r;
+    // the deferred overflow list: scanned before it could outgrow its half
+    // of tlist, and at the end
+    pending += rows;
+    if (c0 + v.gchunk >= end || pending + v.gchunk > GLIST2) {
+      k_gemm_full<TX><<<(unsigned)ss.cus, 1024, 0, s>>>(X, base, d, ldx, k, v,
+                                                       lab_out, acc, flags);
+      if (int r = check_launch("gemm overflow scan")) return r;
+      if (hipMemsetAsync(&v.hdr->gcount2, 0, 4, s) != hipSuccess)
+        return fail(DKM_E_LAUNCH, "gemm: list reset");
+      pending = 0;
+    }
   }
   return 0;
+}
+
+template <class TX>
+int gemm_image(const TX *X, int64_t n, int d, int64_t ldx, const XImage &img,
+               hipStream_t s) {
+  if (n == 0) return 0;
+  return launch_split<TX>(X, 0, n, round_up(n, GT), d, ldx, 1.0,
+                          (char *)img.tiles, (float *)img.xx, 1, s);
 }
 
 template int gemm_screen<double>(const double *, int64_t, int64_t, int,
                                  int64_t, const double *, int, const WsView &,
                                  int32_t *, double *, bool, bool,
-                                 hipStream_t);
+                                 const XImage *, hipStream_t);
 template int gemm_screen<float>(const float *, int64_t, int64_t, int, int64_t,
                                 const double *, int, const WsView &,
-                                int32_t *, double *, bool, bool, hipStream_t);
+                                int32_t *, double *, bool, bool,
+                                const XImage *, hipStream_t);
+template int gemm_image<double>(const double *, int64_t, int, int64_t,
+                                const XImage &, hipStream_t);
+template int gemm_image<float>(const float *, int64_t, int, int64_t,
+                               const XImage &, hipStream_t);
 
 }  // namespace dkm

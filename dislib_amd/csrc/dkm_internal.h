@@ -54,6 +54,8 @@ __host__ __device__ inline int64_t round_up(int64_t a, int64_t b) {
 constexpr int GT = 256;                 // rows per tile (centres or samples)
 constexpr int GBK = 32;                 // features per K-stage
 constexpr int GSTAGE = GT * GBK * 4;    // bytes per operand tile per stage
+// single-product (hi only) tiles: 32-feature stages of 64-B rows
+constexpr int GSTAGE1 = GT * GBK * 2;
 constexpr int GTOP = 4;                 // (score, centre) pairs kept per sample
 
 __host__ __device__ inline int64_t kpad256(int64_t k) { return (k + 255) / 256 * 256; }
@@ -127,8 +129,8 @@ struct WsView {
   float *mind;
   // GEMM screen (gemm_path only; else NULL)
   char *gfrag;     // kpad256 x dpad32 centre tiles (-2c, bf16 hi/lo)
-  char *gfrag1;    // kpad256 x dpad64 centre tiles (-2c, bf16 hi only:
-                   // 64 features per 128-B row, the single-product screen)
+  char *gfrag1;    // kpad256 x dpad32 centre tiles (-2c, bf16 hi only:
+                   // 32 features per 64-B row, the single-product screen)
   float *gcn;      // kpad256 fp32 ||c||^2, 2^100 for padding centres
   char *gxs;       // gemm_chunk samples: split tiles of the current chunk
   float *gxn;      // gemm_chunk fp32 upper bounds of ||x||
@@ -170,10 +172,15 @@ inline bool mind_ok(int64_t k, int64_t d) {
 //    then int32 perm (sample of each image row, -1 past n) and int32 plab
 //    (the current label of each image row: the screen's hints, kept equal
 //    to labels[perm[i]] by the screen and k_plab sync).
-constexpr int IMG_NONE = 0, IMG_SINGLE = 1, IMG_SPLIT = 2, IMG_SORTED = 3;
+//  IMG_GEMM (k_gemm_screen1, d > 128): the single-product GEMM screen's
+//    sample tiles (dkm_gemm.hip layout: 256-row tiles of dpad32(d) / 32
+//    stages x 16 KB, bf16 hi of fl32(x), 64-B rows) over every row, then
+//    fp32 upper bounds of ||x|| (not |x|^2) per row, padding rows 0.
+constexpr int IMG_NONE = 0, IMG_SINGLE = 1, IMG_SPLIT = 2, IMG_SORTED = 3,
+              IMG_GEMM = 4;
 struct XImage {
   const uint16_t *tiles;
-  const float *xx;
+  const float *xx;  // IMG_GEMM: ||x|| bounds
   int kind;
   const int32_t *perm;  // IMG_SORTED only
   int32_t *plab;        // IMG_SORTED only
@@ -448,9 +455,16 @@ int gemm_prepare(const double *C, int64_t k, int64_t d, const WsView &v,
 // Screen samples [base, end): labels (or -(prev + 2) for the exact re-check,
 // counted in hdr->qcount).  acc != NULL: the merge step also moves rows
 // between the sums with fp64 atomics (delta = true: only changed labels).
+// img (IMG_GEMM, or NULL): the resident sample tiles the single-product
+// screen reads instead of splitting X (chunks starting on a 256-row tile)
 template <class TX>
 int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
                 const double *C, int k, const WsView &v, int32_t *lab_out,
-                double *acc, bool delta, bool one, hipStream_t s);
+                double *acc, bool delta, bool one, const XImage *img,
+                hipStream_t s);
+// the IMG_GEMM image of X (x_image_view layout)
+template <class TX>
+int gemm_image(const TX *X, int64_t n, int d, int64_t ldx, const XImage &img,
+               hipStream_t s);
 
 }  // namespace dkm

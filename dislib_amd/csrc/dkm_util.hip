@@ -39,7 +39,7 @@ static size_t gemm_bytes(int64_t k, int64_t d) {
   const int64_t kp = kpad256(k), dp = dpad32(d), m = gemm_chunk(d);
   size_t b = 0;
   b += round_up(kp * dp * 4, 256);              // gfrag
-  b += round_up(kp * dpad64(d) * 2, 256);       // gfrag1
+  b += round_up(kp * dp * 2, 256);              // gfrag1
   b += round_up(kp * 4, 256);                   // gcn
   b += 2 * round_up(m * dp * 4, 256);           // gxs (two chunks)
   b += 2 * round_up(m * 4, 256);                // gxn (two chunks)
@@ -132,7 +132,7 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
     v->gfrag = p;
     p += round_up(kp * dp * 4, 256);
     v->gfrag1 = p;
-    p += round_up(kp * dpad64(d) * 2, 256);
+    p += round_up(kp * dp * 2, 256);
     v->gcn = (float *)p;
     p += round_up(kp * 4, 256);
     v->gxs = p;

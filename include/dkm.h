@@ -133,7 +133,11 @@ int dkm_assign_delta_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
  *     sums exceed LDS; d <= 128);
  *   kind DKM_IMAGE_SPLIT: bf16 hi and lo of fl32(x) for the d <= 32
  *     bf16x3 screen (MODE_SCREEN_BF16X3 or the AUTO choice), read by its
- *     delta / labels-only launches.
+ *     delta / labels-only launches;
+ *   kind DKM_IMAGE_GEMM: bf16(fl32(x)) in the 256-row tiles of the
+ *     single-product GEMM screen (d > 128: MODE_SCREEN_BF16 or AUTO), plus
+ *     an fp32 upper bound of ||x|| per row (2 B per feature + 4 B per row;
+ *     10M x 1024: 20.5 GB).
  * dkm_x_image_kind(k, d, mode) says which kind the selected screen reads
  * (DKM_IMAGE_NONE: building one would be wasted).  The _img forms of
  * dkm_partial_sum / dkm_assign_delta take it (image NULL = none); every
@@ -142,6 +146,7 @@ int dkm_assign_delta_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
 #define DKM_IMAGE_SINGLE 1
 #define DKM_IMAGE_SPLIT 2
 #define DKM_IMAGE_SORTED 3
+#define DKM_IMAGE_GEMM 4
 int dkm_x_image_kind(int64_t k, int64_t d, int mode);
 size_t dkm_x_image_bytes(int64_t n, int64_t d, int kind);
 int dkm_x_image_f64(const double *X, int64_t n, int64_t d, int64_t ldx,

@@ -19,6 +19,7 @@ PT="python -u -m pytest -p no:cacheprovider --timeout 200 --timeout-method threa
 for s in "$@"; do
   case $s in
     t_new) step t_new 600 $PT tests/test_gpu_sorted.py tests/test_gpu_b2.py tests/test_gpu_nonfinite.py tests/test_gpu_fullsize.py ;;
+    t_gemm) step t_gemm 600 $PT tests/test_gpu_gemm.py ;;
     t_nb) step t_nb 600 $PT tests/test_gpu_neighbors.py ;;
     t_c5) step t_c5 600 $PT tests/test_gpu_fullsize.py -k c5 ;;
     t_all) step t_all 900 $PT -m gpu tests ;;
@@ -32,6 +33,11 @@ for s in "$@"; do
       cut -c1-300 $P/iters.txt ;;
     c3ns) DKM_SORTED_IMAGE=0 step c3ns 300 python bench.py --n 125000000 --d 64 --k 1000 --steps 8 --warmup 2 --no-cpu --only-headline ;;
     c4) step c4 300 python bench.py --n 10000000 --d 1024 --k 4096 --steps 4 --warmup 2 --no-cpu --only-headline ;;
+    c4it) P=$OUT/${TAG}_c4it; mkdir -p $P
+      step c4it 300 rocprofv3 --kernel-trace --stats -d $P -o run -- python bench.py --n 10000000 --d 1024 --k 4096 --steps 4 --warmup 2 --no-cpu --only-headline
+      DB=$(find $P -name '*.db' | head -1)
+      [ -n "$DB" ] && python tools/prof_iters.py $DB > $P/iters.txt 2>&1 && rm -f $DB
+      cut -c1-400 $P/iters.txt ;;
     c4prof) step c4prof 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/${TAG}_c4prof -o run -- python bench.py --n 10000000 --d 1024 --k 4096 --steps 4 --warmup 2 --no-cpu --only-headline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
