@@ -20,6 +20,8 @@ run() {  # name counters...
   timeout -k 10 240 rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
      -d $OUT/$name -o run -- "${PROG[@]}" > $OUT/$name.log 2>&1
   local rc=$?; echo "== rc=$rc"; tail -2 $OUT/$name.log
+  # keep only the counter tables (the pull-back is capped at 64 MiB)
+  find $OUT/$name -type f ! -name '*counter_collection.csv' -delete 2>/dev/null
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo STOP; exit $rc; fi
 }
 run p1 SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE
