@@ -25,16 +25,18 @@
 //                  lane per 32-centre pass, 16-B loads of the fp32 C^T
 //                  (d x ct_ld(k)); the row's entries staged 8 at a time in
 //                  the group's lanes and walked by ds_bpermute.  Per centre
-//                  j: s_j = |c_j|^2 - 2 x.c_j (fp32 fma chain), the bound
-//                  B_j from sum |x||c_j| (below), and the slice's state
-//                  (s1, s1 - B1, s1 + B1, c1, min over others of s_j - B_j).
+//                  j only s_j = |c_j|^2 - 2 x.c_j (one fp32 fma per stored
+//                  entry); the slice's state is its two smallest scores and
+//                  the index of the first; the bound B (below) is one per
+//                  sample.
 //   k_csr_merge    one lane per sample: the slices' states merged (ascending
 //                  centre ranges: a strict < keeps the first index); decided
-//                  when s1 + B1 < s_j - B_j for every other j -- then the
-//                  reference's fp64 distances order the same way, strictly,
-//                  also after sqrt -- else listed for k_csr_resolve.  Writes
-//                  the label and, on the incremental path, moves the rows
-//                  whose label changed (+x new, -x previous; fp64 atomics).
+//                  when s1 + B < s2 - B for the best s1 and the next s2 --
+//                  then the reference's fp64 distances order the same way,
+//                  strictly, also after sqrt -- else listed for
+//                  k_csr_resolve.  Writes the label and, on the incremental
+//                  path, moves the rows whose label changed (+x new,
+//                  -x previous; fp64 atomics).
 //   k_csr_resolve  a wave per listed sample: the reference arithmetic over
 //                  all k centres (fp64 C^T), first-index argmin.
 //   k_csr_seg_sums the full [sums | counts]: samples counting-sorted by
@@ -45,15 +47,21 @@
 // workspace tail (20 bytes per slice and sample).
 //
 // The bound.  With u = 2^-24 (fp32) and w = 2^-53 (fp64), n stored entries,
-// A_j >= sum |x_v c_jv| (accumulated beside the dot) and M_j = xx + |c_j|^2
-// + 2 A_j + |s_j| >= the magnitude of every partial result:
+// A_j >= sum |x_v c_jv| and M_j = xx + |c_j|^2 + 2 A_j + |s_j| >= the
+// magnitude of every partial result:
 //   fp32 dot vs exact          (n + 2) u A_j     (inputs rounded, fma chain)
 //   sklearn's fp64 dot         n w A_j
 //   s_j rounding, |c|^2 -> fp32  u |s_j| + u |c_j|^2
 //   sklearn's two additions    2 w M_j;  sqrt strictly monotone: 4 w M_j
 // B_j = 2 x their sum (+ 2^-100 absolute, for underflow): s1 + B1 < s_j - B_j
 // implies S_1 < S_j with a margin that survives sqrt, where S = sklearn's
-// squared distances.  NaN/inf anywhere makes a sample undecided.
+// squared distances.  The screen uses one B >= every B_j per sample, from
+// A_j <= ||x|| ||c_j|| (Cauchy-Schwarz), ||c_j|| <= cmax = max_j ||c_j|| and
+// |s_j| <= |c_j|^2 + 2 A_j: no per-centre |x||c| sums, which doubled the
+// screen's VALU work (C5: 11.7 -> 10.4 ms per step, every sample still
+// decided), at a bound a few times looser than the per-centre one.  NaN /
+// inf anywhere (a centre norm, an overflowing score) makes B or the scores
+// non-finite: undecided.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -76,7 +84,7 @@ constexpr int CSR_SUMB = 1024;
 enum { OP_PREDICT = 0, OP_FULL = 1, OP_DELTA = 2, OP_FULL_ATOMIC = 3 };
 
 struct SliceState {
-  float s1, lo1, hi1, lo2;
+  float s1, s2;  // the slice's smallest score and the next one
 };
 
 __device__ __forceinline__ int lane_prefix64(uint64_t m) {
@@ -99,7 +107,10 @@ __device__ __forceinline__ void add_row(const int64_t *indptr,
 
 // NP passes of 32 centres per walk over the entries (a slice wider than
 // 32 * NP centres is walked again).  Slice s covers centres
-// [s * ks, min(k, (s + 1) * ks)), ks a multiple of 32.
+// [s * ks, min(k, (s + 1) * ks)), ks a multiple of 32.  Per centre only the
+// fp32 score s_j = |c_j|^2 - 2 x.c_j (one fma per stored entry); the bound
+// B is one per sample (the header comment), so a lane keeps its two
+// smallest scores and the index of the smallest.
 template <int NP>
 __global__ void __launch_bounds__(CSR_BLOCK)
     k_csr_screen(const int64_t *__restrict__ indptr,
@@ -107,8 +118,9 @@ __global__ void __launch_bounds__(CSR_BLOCK)
                  const double *__restrict__ data, int64_t i0, int64_t m,
                  const float *__restrict__ CT, int64_t dct,
                  const float *__restrict__ cn, int k, int S, int ks,
+                 const WsHeader *__restrict__ hdr,
                  SliceState *__restrict__ pst, int32_t *__restrict__ pidx,
-                 float *__restrict__ pxx) {
+                 float *__restrict__ pxx, float *__restrict__ pb) {
   const int lane = threadIdx.x & 63, sg = lane / CSR_G, gl = lane % CSR_G;
   const int gbase = sg * CSR_G;
   const int s = blockIdx.x % S;
@@ -118,21 +130,24 @@ __global__ void __launch_bounds__(CSR_BLOCK)
   const int j_lo = s * ks, j_hi = min(k, j_lo + ks);
   // this slice's d x ks block of the sliced fp32 C^T
   const float *CTs = CT + (int64_t)s * dct * ks - j_lo;
+  // max_j ||c_j|| (fp64, ordered bits), rounded up to fp32
+  const float cmax =
+      (float)__longlong_as_double((long long)hdr->cmax_bits) * 1.000001f;
   for (int64_t q0 = wv * CSR_SPW; q0 < m; q0 += nwv * CSR_SPW) {
     const int64_t q = q0 + sg;
     const bool live = q < m;
     const int64_t a = live ? indptr[i0 + q] : 0;
     const int64_t b = live ? indptr[i0 + q + 1] : 0;
     const float nf = (float)(b - a);
-    SliceState st{INFINITY, INFINITY, INFINITY, INFINITY};
+    float s1 = INFINITY, s2 = INFINITY;
     int i1 = 0x7fffffff;
     float xx = 0.f;
     for (int jp = j_lo; jp < j_hi; jp += CSR_PASS * NP) {
-      float dot[NP][4], adot[NP][4];
+      float dot[NP][4];
 #pragma unroll
       for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int h = 0; h < 4; ++h) dot[p][h] = adot[p][h] = 0.f;
+        for (int h = 0; h < 4; ++h) dot[p][h] = 0.f;
       const bool first = jp == j_lo;
       for (int64_t c0 = a; c0 < b; c0 += CSR_G) {
         const int cnt = (int)min<int64_t>(CSR_G, b - c0);
@@ -142,14 +157,15 @@ __global__ void __launch_bounds__(CSR_BLOCK)
           myi = indices[c0 + gl];
           myv = (float)data[c0 + gl];
         }
-        // the chunk's C^T row loads first, then the adds
+        // the chunk's C^T row loads first, then the fmas
         float4 cv[CSR_G][NP];
         float vv[CSR_G];
 #pragma unroll
         for (int e = 0; e < CSR_G; ++e) {
           const int idx = __shfl(myi, gbase + e, WAVE);
           vv[e] = __shfl(myv, gbase + e, WAVE);
-          const float *row = CTs + (int64_t)idx * ks + jp + 4 * gl;
+          // element offset < 2^31: d x ks floats per slice
+          const float *row = CTs + (uint32_t)(idx * ks + jp + 4 * gl);
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
             const int j = jp + CSR_PASS * p + 4 * gl;
@@ -161,73 +177,67 @@ __global__ void __launch_bounds__(CSR_BLOCK)
 #pragma unroll
         for (int e = 0; e < CSR_G; ++e) {
           if (e < cnt) {
-            const float v = vv[e], av = fabsf(v);
+            const float v = vv[e];
             if (first) xx = fmaf(v, v, xx);
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
-              const float c4[4] = {cv[e][p].x, cv[e][p].y, cv[e][p].z,
-                                   cv[e][p].w};
-#pragma unroll
-              for (int h = 0; h < 4; ++h) {
-                dot[p][h] = fmaf(v, c4[h], dot[p][h]);
-                adot[p][h] = fmaf(av, fabsf(c4[h]), adot[p][h]);
-              }
+              dot[p][0] = fmaf(v, cv[e][p].x, dot[p][0]);
+              dot[p][1] = fmaf(v, cv[e][p].y, dot[p][1]);
+              dot[p][2] = fmaf(v, cv[e][p].z, dot[p][2]);
+              dot[p][3] = fmaf(v, cv[e][p].w, dot[p][3]);
             }
           }
         }
       }
-      const float xx_up = xx * (1.f + (nf + 4.f) * 0x1.0p-23f);
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
           const int j = jp + CSR_PASS * p + 4 * gl + h;
-          if (j < j_hi) {
-            const float cj = cn[j];
-            const float sj = fmaf(-2.f, dot[p][h], cj);
-            const float as = fabsf(sj), A = adot[p][h];
-            const float M = xx_up + cj + 2.f * A + as;
-            const float B = 0x1.0p-23f * (cj + as + 2.f * (nf + 2.f) * A) +
-                            (2.f * nf + 6.f) * 0x1.0p-52f * M + 0x1.0p-100f;
-            float lo = sj - B;
-            const float hi = sj + B;
-            if (!(lo == lo) || !(hi < INFINITY)) lo = -INFINITY;  // poison
-            if (sj < st.s1) {
-              st.lo2 = fminf(st.lo2, st.lo1);
-              st.s1 = sj;
-              st.lo1 = lo;
-              st.hi1 = hi;
+          if (j < j_hi) {  // centres ascending per lane: strict < = first
+            const float sj = fmaf(-2.f, dot[p][h], cn[j]);
+            if (sj < s1) {
+              s2 = s1;
+              s1 = sj;
               i1 = j;
             } else {
-              st.lo2 = fminf(st.lo2, lo);
+              s2 = fminf(s2, sj);
             }
           }
         }
       }
     }
-    // a lane whose centres were all NaN keeps i1 = none: poison the slice
-    if (j_lo < j_hi && i1 == 0x7fffffff) st.lo2 = -INFINITY;
 #pragma unroll
     for (int off = CSR_G / 2; off >= 1; off >>= 1) {
-      SliceState o;
-      o.s1 = __shfl_xor(st.s1, off, WAVE);
-      o.lo1 = __shfl_xor(st.lo1, off, WAVE);
-      o.hi1 = __shfl_xor(st.hi1, off, WAVE);
-      o.lo2 = __shfl_xor(st.lo2, off, WAVE);
+      const float o1 = __shfl_xor(s1, off, WAVE);
+      const float o2 = __shfl_xor(s2, off, WAVE);
       const int oi = __shfl_xor(i1, off, WAVE);
-      const bool take = o.s1 < st.s1 || (o.s1 == st.s1 && oi < i1);
+      const bool take = o1 < s1 || (o1 == s1 && oi < i1);
+      s2 = fminf(fminf(s2, o2), take ? s1 : o1);
       if (take) {
-        o.lo2 = fminf(fminf(o.lo2, st.lo2), st.lo1);
-        st = o;
+        s1 = o1;
         i1 = oi;
-      } else {
-        st.lo2 = fminf(fminf(st.lo2, o.lo2), o.lo1);
       }
     }
     if (live && gl == 0) {
-      pst[(int64_t)s * m + q] = st;
+      pst[(int64_t)s * m + q] = SliceState{s1, s2};
       pidx[(int64_t)s * m + q] = i1;
-      if (s == 0) pxx[q] = xx * (1.f - (nf + 4.f) * 0x1.0p-23f);
+      if (s == 0) {
+        // the bound of every centre of the sample (header comment): A >=
+        // sum |x_v c_jv| by Cauchy-Schwarz, |c_j|^2 <= cmax^2, |s_j| <=
+        // |c_j|^2 + 2A; doubled, + 2^-100 for underflow; NaN / inf: no
+        // decision
+        const float xx_up = xx * (1.f + (nf + 4.f) * 0x1.0p-23f);
+        const float A = sqrtf(xx_up) * cmax * (1.f + 0x1.0p-20f);
+        const float c2 = cmax * cmax * (1.f + 0x1.0p-22f);
+        const float M = xx_up + 2.f * c2 + 4.f * A;
+        const float B = (0x1.0p-23f * (2.f * c2 + 2.f * A +
+                                       2.f * (nf + 2.f) * A) +
+                         (2.f * nf + 6.f) * 0x1.0p-52f * M + 0x1.0p-100f) *
+                        (1.f + 0x1.0p-20f);
+        pxx[q] = xx * (1.f - (nf + 4.f) * 0x1.0p-23f);
+        pb[q] = B;
+      }
     }
   }
 }
@@ -240,8 +250,9 @@ __global__ void __launch_bounds__(256)
                 const double *__restrict__ data, int64_t i0, int64_t m, int d,
                 int k, int S, const SliceState *__restrict__ pst,
                 const int32_t *__restrict__ pidx,
-                const float *__restrict__ pxx, int32_t *labels, double *acc,
-                int op, int32_t *__restrict__ list, uint32_t *nlist) {
+                const float *__restrict__ pxx, const float *__restrict__ pb,
+                int32_t *labels, double *acc, int op,
+                int32_t *__restrict__ list, uint32_t *nlist) {
   const int lane = threadIdx.x & 63;
   for (int64_t q0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63);
        q0 < m; q0 += (int64_t)gridDim.x * blockDim.x) {
@@ -250,21 +261,25 @@ __global__ void __launch_bounds__(256)
     if (q < m) {
       SliceState w = pst[q];
       int wi = pidx[q];
-      float L = w.lo2;
-      for (int s = 1; s < S; ++s) {
-        const SliceState t = pst[(int64_t)s * m + q];
-        const int ti = pidx[(int64_t)s * m + q];
+      float s2 = w.s2;  // the smallest score but the best, over the slices
+      for (int sl = 1; sl < S; ++sl) {
+        const SliceState t = pst[(int64_t)sl * m + q];
+        const int ti = pidx[(int64_t)sl * m + q];
         if (ti != 0x7fffffff &&
             (wi == 0x7fffffff || t.s1 < w.s1 || (t.s1 == w.s1 && ti < wi))) {
-          L = fminf(fminf(L, w.lo1), t.lo2);
+          s2 = fminf(fminf(s2, w.s1), t.s2);
           w = t;
           wi = ti;
         } else {
-          L = fminf(fminf(L, t.lo1), t.lo2);
+          s2 = fminf(fminf(s2, t.s1), t.s2);
         }
       }
+      const float B = pb[q];
+      const float L = s2 - B;
+      // every other centre's fp64 distance^2 provably exceeds the best's
+      // (strictly, also after sqrt), and the clamp at 0 cannot tie them
       const bool decided =
-          wi != 0x7fffffff && w.hi1 < L && pxx[q] + L > 0.f;
+          wi != 0x7fffffff && w.s1 + B < L && pxx[q] + L > 0.f;
       const int64_t i = i0 + q;
       const int prev = (op == OP_DELTA) ? labels[i] : -1;
       if (decided) {
@@ -451,16 +466,18 @@ static int csr_run(const int64_t *indptr, const int32_t *indices,
     op = OP_FULL_ATOMIC;  // no label array to sort (or k beyond the sort)
   const int S = csr_slices(k, d);
   const int ks = (int)csr_slice_width(k, d);
-  // per chunk sample: S slice states (20 B), x.x bound (4 B), list slot (4 B)
+  // per chunk sample: S slice states (12 B), x.x and B bounds (8 B), list
+  // slot (4 B)
   const int64_t chunk =
-      std::min<int64_t>(n, v.nq * 12 / (20 * S + 8));
+      std::min<int64_t>(n, v.nq * 12 / (12 * S + 12));
   if (chunk <= 0)
     return fail(DKM_E_WORKSPACE, std::string(who) + ": workspace too small");
   char *tail = (char *)v.queue;
   SliceState *pst = (SliceState *)tail;
   int32_t *pidx = (int32_t *)(pst + (int64_t)S * chunk);
   float *pxx = (float *)(pidx + (int64_t)S * chunk);
-  int32_t *list = (int32_t *)(pxx + chunk);
+  float *pb = pxx + chunk;
+  int32_t *list = (int32_t *)(pb + chunk);
   uint32_t *nlist = &v.hdr->csr_nund;
   hipStream_t st = (hipStream_t)stream;
   const int cu = csr_cus();
@@ -475,7 +492,8 @@ static int csr_run(const int64_t *indptr, const int32_t *indices,
 #define DKM_SCREEN(NP)                                                       \
   k_csr_screen<NP><<<g, CSR_BLOCK, 0, st>>>(indptr, indices, data, i0, m,   \
                                             v.ct32, d, v.cn32,              \
-                                            (int)k, S, ks, pst, pidx, pxx)
+                                            (int)k, S, ks, v.hdr, pst,      \
+                                            pidx, pxx, pb)
     if (npass >= 2)
       DKM_SCREEN(2);
     else
@@ -486,8 +504,8 @@ static int csr_run(const int64_t *indptr, const int32_t *indices,
     const unsigned gm = (unsigned)std::max<int64_t>(
         1, std::min<int64_t>((m + 255) / 256, (int64_t)cu * 16));
     k_csr_merge<<<gm, 256, 0, st>>>(indptr, indices, data, i0, m, (int)d,
-                                    (int)k, S, pst, pidx, pxx, labels, acc,
-                                    op, list, nlist);
+                                    (int)k, S, pst, pidx, pxx, pb, labels,
+                                    acc, op, list, nlist);
     k_csr_resolve<<<(unsigned)cu * 4, 256, 0, st>>>(
         indptr, indices, data, i0, (int)d, v.ct64, ct_ld(k), v.cn64, (int)k,
         labels, acc, op, list, nlist,

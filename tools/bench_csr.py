@@ -82,7 +82,8 @@ def main():
            "gather_tbs": 4 * nnz * a.k / (el / a.steps) / 1e12,
            "full_sums_iteration_ms": full_ms,
            "predict_ms": pred_ms,
-           "predict_samples_per_s": a.n / (pred_ms * 1e-3)}
+           "predict_samples_per_s": a.n / (pred_ms * 1e-3),
+           "rechecked_total": st.rechecked()}
     print(json.dumps(out))
 
 
