@@ -133,11 +133,39 @@ __global__ void __launch_bounds__(CSR_BLOCK)
   // max_j ||c_j|| (fp64, ordered bits), rounded up to fp32
   const float cmax =
       (float)__longlong_as_double((long long)hdr->cmax_bits) * 1.000001f;
+  // Software pipeline over the wave's 8-sample groups: the next group's row
+  // bounds load at the start of a group, its first 2 x 8 (index, value)
+  // pairs at the end, so a group's gathers wait on no other load.
+  int64_t a_nx = 0, b_nx = 0;
+  int pi[2] = {0, 0};
+  float pv[2] = {0.f, 0.f};
+  auto load_pairs = [&](int64_t a0, int64_t b0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t t = a0 + CSR_G * u + gl;
+      pi[u] = t < b0 ? indices[t] : 0;
+      pv[u] = t < b0 ? (float)data[t] : 0.f;
+    }
+  };
+  {
+    const int64_t q = wv * CSR_SPW + sg;
+    if (q < m) {
+      a_nx = indptr[i0 + q];
+      b_nx = indptr[i0 + q + 1];
+    }
+    load_pairs(a_nx, b_nx);
+  }
   for (int64_t q0 = wv * CSR_SPW; q0 < m; q0 += nwv * CSR_SPW) {
     const int64_t q = q0 + sg;
     const bool live = q < m;
-    const int64_t a = live ? indptr[i0 + q] : 0;
-    const int64_t b = live ? indptr[i0 + q + 1] : 0;
+    const int64_t a = a_nx, b = b_nx;
+    const int ci[2] = {pi[0], pi[1]};
+    const float cvv[2] = {pv[0], pv[1]};
+    {
+      const int64_t qn = q + nwv * CSR_SPW;
+      a_nx = qn < m ? indptr[i0 + qn] : 0;
+      b_nx = qn < m ? indptr[i0 + qn + 1] : 0;
+    }
     const float nf = (float)(b - a);
     float s1 = INFINITY, s2 = INFINITY;
     int i1 = 0x7fffffff;
@@ -149,11 +177,24 @@ __global__ void __launch_bounds__(CSR_BLOCK)
 #pragma unroll
         for (int h = 0; h < 4; ++h) dot[p][h] = 0.f;
       const bool first = jp == j_lo;
+      // the pass's |c_j|^2 load early (used after the gathers)
+      float cnv[NP][4];
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int j = jp + CSR_PASS * p + 4 * gl + h;
+          cnv[p][h] = j < j_hi ? cn[j] : 0.f;
+        }
       for (int64_t c0 = a; c0 < b; c0 += CSR_G) {
         const int cnt = (int)min<int64_t>(CSR_G, b - c0);
+        const int64_t u = (c0 - a) / CSR_G;
         int myi = 0;
         float myv = 0.f;
-        if (gl < cnt) {
+        if (u < 2) {  // group-uniform: the pipelined pairs
+          myi = u ? ci[1] : ci[0];
+          myv = u ? cvv[1] : cvv[0];
+        } else if (gl < cnt) {
           myi = indices[c0 + gl];
           myv = (float)data[c0 + gl];
         }
@@ -195,7 +236,7 @@ __global__ void __launch_bounds__(CSR_BLOCK)
         for (int h = 0; h < 4; ++h) {
           const int j = jp + CSR_PASS * p + 4 * gl + h;
           if (j < j_hi) {  // centres ascending per lane: strict < = first
-            const float sj = fmaf(-2.f, dot[p][h], cn[j]);
+            const float sj = fmaf(-2.f, dot[p][h], cnv[p][h]);
             if (sj < s1) {
               s2 = s1;
               s1 = sj;
@@ -207,6 +248,7 @@ __global__ void __launch_bounds__(CSR_BLOCK)
         }
       }
     }
+    load_pairs(a_nx, b_nx);  // the next group's first 16 pairs
 #pragma unroll
     for (int off = CSR_G / 2; off >= 1; off >>= 1) {
       const float o1 = __shfl_xor(s1, off, WAVE);
