@@ -85,14 +85,14 @@ SIGNATURES = {
     "dkm_knn_f64": (_i32, [_p, _i64, _i64, _p, _i64, _i64, _i64, _i64, _p,
                            _sz, _p, _p, _p]),
     "dkm_knn_csr_f64": (_i32, [_p, _p, _p, _i64, _p, _p, _p, _i64, _i64,
-                               _i64, _p, _sz, _p, _p, _p]),
+                               _i64, _i32, _p, _sz, _p, _p, _p]),
     "dkm_radius_count_f64": (_i32, [_p, _i64, _i64, _p, _i64, _i64, _i64,
                                     _f64, _p, _p]),
     "dkm_radius_workspace_bytes": (_sz, [_i64, _i64]),
     "dkm_radius_count_csr_f64": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64,
-                                        _f64, _p, _p]),
+                                        _f64, _i32, _p, _p]),
     "dkm_radius_fill_csr_f64": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64,
-                                       _f64, _p, _p, _sz, _p, _p, _p]),
+                                       _f64, _i32, _p, _p, _sz, _p, _p, _p]),
     "dkm_radius_fill_f64": (_i32, [_p, _i64, _i64, _p, _i64, _i64, _i64,
                                    _f64, _p, _p, _sz, _p, _p, _p]),
     # multi-GPU all-reduce (RCCL)

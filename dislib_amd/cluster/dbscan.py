@@ -92,9 +92,11 @@ def _compute_neighbours_csr(epsilon, min_samples, begin_idx, end_idx,
             indices = t.zeros(1, dtype=t.int32, device=dev)
             data = t.zeros(1, dtype=t.float64, device=dev)
         counts = t.empty(nq, dtype=t.int64, device=dev)
+        f32 = 1 if getattr(m, "dkm_f32", False) else 0
         _lib.check(so.dkm_radius_count_csr_f64(
             ptr(indptr), ptr(indices), ptr(data), n, d, b, nq,
-            float(epsilon), ptr(counts), stream_ptr()), "dkm_radius_count_csr")
+            float(epsilon), f32, ptr(counts), stream_ptr()),
+            "dkm_radius_count_csr")
         c = counts.cpu().numpy()
         offsets = np.concatenate([[0], np.cumsum(c)]).astype(np.int64)
         total = int(offsets[-1])
@@ -105,8 +107,9 @@ def _compute_neighbours_csr(epsilon, min_samples, begin_idx, end_idx,
         ws = t.empty(wsb, dtype=t.uint8, device=dev)
         _lib.check(so.dkm_radius_fill_csr_f64(
             ptr(indptr), ptr(indices), ptr(data), n, d, b, nq,
-            float(epsilon), ptr(off_d), ctypes.c_void_p(ws.data_ptr()), wsb,
-            ptr(out_i), ptr(out_d), stream_ptr()), "dkm_radius_fill_csr")
+            float(epsilon), f32, ptr(off_d), ctypes.c_void_p(ws.data_ptr()),
+            wsb, ptr(out_i), ptr(out_d), stream_ptr()),
+            "dkm_radius_fill_csr")
         idx = out_i[:total].cpu().numpy()
     neigh = [idx[offsets[i]:offsets[i + 1]] for i in range(nq)]
     core = [bool(c[i] >= min_samples) for i in range(nq)]
@@ -128,7 +131,9 @@ def _concat_csr(subsets, who="compute_neighbours"):
             raise ValueError("%s: sparse=True needs sparse Subsets" % who)
         parts.append(x)
     m = sp.csr_matrix(parts[0] if len(parts) == 1 else
-                      sp.vstack(parts, format="csr"), dtype=np.float64)
+                      sp.vstack(parts, format="csr"))
+    f32 = m.dtype == np.float32   # sklearn's float32 (upcast) path
+    m = sp.csr_matrix(m, dtype=np.float64)
     if not m.has_sorted_indices:
         m = m.sorted_indices()
     if m.shape[1] > np.iinfo(np.int32).max:
@@ -148,6 +153,7 @@ def _concat_csr(subsets, who="compute_neighbours"):
                     "%s: sparse samples hold duplicate column entries; call "
                     "sum_duplicates() on them first" % who)
     _device_assert_finite(m.data)
+    m.dkm_f32 = bool(f32)
     return m
 
 

@@ -169,8 +169,8 @@ __global__ void __launch_bounds__(NB)
                    const int64_t *__restrict__ xp,
                    const int32_t *__restrict__ xi,
                    const double *__restrict__ xd, int64_t nx, int64_t plen,
-                   int P, double *__restrict__ pr, int *__restrict__ pi,
-                   const double *__restrict__ flr,
+                   int P, int f32, double *__restrict__ pr,
+                   int *__restrict__ pi, const double *__restrict__ flr,
                    const int *__restrict__ fli) {
   const int lane = threadIdx.x & 63;
   const int64_t qg = (int64_t)blockIdx.x * (NB / 64) +
@@ -210,7 +210,12 @@ __global__ void __launch_bounds__(NB)
     double r = -2.0 * dot;
     r += xx;
     r += yy;
-    r = r < 0.0 ? 0.0 : r;
+    if (f32) {  // float32 Subsets: the squares rounded to float32 first
+      const float r32 = (float)r;
+      r = r32 < 0.f ? 0.0 : (double)r32;
+    } else {
+      r = r < 0.0 ? 0.0 : r;
+    }
     // a later pass: only (r, j) strictly after the previous pass's last
     if (r > fr || (r == fr && (int)j > fi)) top.push(r, (int)j);
   }
@@ -229,7 +234,7 @@ __global__ void __launch_bounds__(NB)
     k_knn_merge(const double *__restrict__ pr, const int *__restrict__ pi,
                 int64_t nq, int P, int kn, double *__restrict__ out_d,
                 int64_t *__restrict__ out_i, int64_t ldo,
-                double *__restrict__ flr, int *__restrict__ fli) {
+                double *__restrict__ flr, int *__restrict__ fli, int f32) {
   const int64_t q = (int64_t)blockIdx.x * NB + threadIdx.x;
   if (q >= nq) return;
   TopK<K> top;
@@ -247,7 +252,9 @@ __global__ void __launch_bounds__(NB)
 #pragma unroll
   for (int s = 0; s < K; ++s)
     if (s < kn) {
-      out_d[q * ldo + s] = sqrt(top.r[s]);
+      // f32: r is a float32 value; the fp64 sqrt rounds to float32's own
+      out_d[q * ldo + s] = f32 ? (double)(float)sqrt(top.r[s])
+                               : sqrt(top.r[s]);
       out_i[q * ldo + s] = (int64_t)top.i[s];
       if (s == kn - 1) {  // where the next pass starts
         flr[q] = top.r[s];
@@ -328,7 +335,7 @@ __global__ void __launch_bounds__(NB)
     k_radius_csr(const int64_t *__restrict__ indptr,
                  const int32_t *__restrict__ indices,
                  const double *__restrict__ data, int64_t q0, int64_t nq,
-                 int64_t nx, double eps, int64_t plen,
+                 int64_t nx, double eps, int64_t plen, int f32,
                  unsigned long long *__restrict__ cnt,
                  int64_t *__restrict__ out_i, double *__restrict__ out_d) {
   const int lane = threadIdx.x & 63;
@@ -338,6 +345,7 @@ __global__ void __launch_bounds__(NB)
   const int64_t q = qg * 64 + lane;
   if (qg * 64 >= nq) return;
   const bool live = q < nq;
+  const float eps32 = (float)eps;  // numpy compares float32 in float32
   const int64_t qa = live ? indptr[q0 + q] : 0;
   const int64_t qb = live ? indptr[q0 + q + 1] : 0;
   double xx = 0.0;
@@ -369,15 +377,29 @@ __global__ void __launch_bounds__(NB)
     double r = -2.0 * dot;
     r += xx;
     r += yy;
-    r = r < 0.0 ? 0.0 : r;  // np.maximum(r, 0): NaN stays NaN
-    const bool in = r < e2lo || (r <= e2hi && sqrt(r) < eps);
+    double dist;
+    bool in;
+    if (f32) {
+      // float32 Subsets: sklearn's upcast path rounds the fp64 squares to
+      // float32, then max and sqrt in float32 (correctly rounded: the fp64
+      // sqrt of a float rounds to the float32 sqrt)
+      float r32 = (float)r;
+      r32 = r32 < 0.f ? 0.f : r32;
+      const float d32 = (float)sqrt((double)r32);
+      dist = d32;
+      in = d32 < eps32;
+    } else {
+      r = r < 0.0 ? 0.0 : r;  // np.maximum(r, 0): NaN stays NaN
+      dist = sqrt(r);
+      in = r < e2lo || (r <= e2hi && dist < eps);
+    }
     if (live && in) {
       if constexpr (PASS == 0) {
         ++mine;
       } else {
         const unsigned long long at = atomicAdd(cnt + q, 1ull);
         out_i[at] = j;
-        out_d[at] = sqrt(r);
+        out_d[at] = dist;
       }
     }
   }
@@ -569,10 +591,10 @@ template <int K>
 int knn_csr_launch(dim3 g, hipStream_t s, const int64_t *qp,
                    const int32_t *qi, const double *qd, int64_t nq,
                    const int64_t *xp, const int32_t *xi, const double *xd,
-                   int64_t nx, int64_t plen, int P, double *pr, int *pi,
-                   const double *flr, const int *fli) {
+                   int64_t nx, int64_t plen, int P, int f32, double *pr,
+                   int *pi, const double *flr, const int *fli) {
   k_knn_csr_part<K><<<g, NB, 0, s>>>(qp, qi, qd, nq, xp, xi, xd, nx, plen, P,
-                                     pr, pi, flr, fli);
+                                     f32, pr, pi, flr, fli);
   return check_launch("knn csr partial lists");
 }
 
@@ -580,15 +602,15 @@ int knn_csr_launch(dim3 g, hipStream_t s, const int64_t *qp,
 // of out starting at c0)
 int knn_merge_launch(int K, hipStream_t s, const double *pr, const int *pi,
                      int64_t nq, int P, int kk, double *od, int64_t *oi,
-                     int64_t ldo, double *flr, int *fli) {
+                     int64_t ldo, double *flr, int *fli, int f32) {
   const unsigned gm = (unsigned)((nq + NB - 1) / NB);
   switch (K) {
-    case 1: k_knn_merge<1><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
-    case 2: k_knn_merge<2><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
-    case 4: k_knn_merge<4><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
-    case 8: k_knn_merge<8><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
-    case 16: k_knn_merge<16><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
-    default: k_knn_merge<32><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli); break;
+    case 1: k_knn_merge<1><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli, f32); break;
+    case 2: k_knn_merge<2><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli, f32); break;
+    case 4: k_knn_merge<4><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli, f32); break;
+    case 8: k_knn_merge<8><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli, f32); break;
+    case 16: k_knn_merge<16><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli, f32); break;
+    default: k_knn_merge<32><<<gm, NB, 0, s>>>(pr, pi, nq, P, kk, od, oi, ldo, flr, fli, f32); break;
   }
   return check_launch("knn merge");
 }
@@ -710,7 +732,7 @@ int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
     }
     if (r) return r;
     if (int e = knn_merge_launch(K, s, pr, pi, nq, P, kk, out_dist + c0,
-                                 out_idx + c0, kn, flr, fli))
+                                 out_idx + c0, kn, flr, fli, 0))
       return e;
   }
   return 0;
@@ -719,7 +741,7 @@ int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
 int dkm_knn_csr_f64(const int64_t *q_indptr, const int32_t *q_indices,
                     const double *q_data, int64_t nq, const int64_t *x_indptr,
                     const int32_t *x_indices, const double *x_data,
-                    int64_t nx, int64_t d, int64_t kn, void *ws,
+                    int64_t nx, int64_t d, int64_t kn, int out_f32, void *ws,
                     size_t ws_bytes, double *out_dist, int64_t *out_idx,
                     void *stream) {
   if (nq < 0 || nx < 1 || d < 1 || d > INT32_MAX || nx > INT32_MAX)
@@ -753,16 +775,16 @@ int dkm_knn_csr_f64(const int64_t *q_indptr, const int32_t *q_indices,
     const int *fi = c0 ? fli : nullptr;
     int r;
     switch (K) {
-      case 1: r = knn_csr_launch<1>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
-      case 2: r = knn_csr_launch<2>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
-      case 4: r = knn_csr_launch<4>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
-      case 8: r = knn_csr_launch<8>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
-      case 16: r = knn_csr_launch<16>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
-      default: r = knn_csr_launch<32>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, pr, pi, fr, fi); break;
+      case 1: r = knn_csr_launch<1>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, out_f32 ? 1 : 0, pr, pi, fr, fi); break;
+      case 2: r = knn_csr_launch<2>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, out_f32 ? 1 : 0, pr, pi, fr, fi); break;
+      case 4: r = knn_csr_launch<4>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, out_f32 ? 1 : 0, pr, pi, fr, fi); break;
+      case 8: r = knn_csr_launch<8>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, out_f32 ? 1 : 0, pr, pi, fr, fi); break;
+      case 16: r = knn_csr_launch<16>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, out_f32 ? 1 : 0, pr, pi, fr, fi); break;
+      default: r = knn_csr_launch<32>(g, s, q_indptr, q_indices, q_data, nq, x_indptr, x_indices, x_data, nx, plen, P, out_f32 ? 1 : 0, pr, pi, fr, fi); break;
     }
     if (r) return r;
     if (int e = knn_merge_launch(K, s, pr, pi, nq, P, kk, out_dist + c0,
-                                 out_idx + c0, kn, flr, fli))
+                                 out_idx + c0, kn, flr, fli, out_f32 ? 1 : 0))
       return e;
   }
   return 0;
@@ -832,7 +854,7 @@ int dkm_radius_fill_f64(const double *Q, int64_t nq, int64_t ldq,
 
 int dkm_radius_count_csr_f64(const int64_t *indptr, const int32_t *indices,
                              const double *data, int64_t n, int64_t d,
-                             int64_t q0, int64_t nq, double eps,
+                             int64_t q0, int64_t nq, double eps, int out_f32,
                              int64_t *counts, void *stream) {
   if (int r = radius_csr_args(indptr, indices, data, n, d, q0, nq, eps))
     return r;
@@ -846,14 +868,15 @@ int dkm_radius_count_csr_f64(const int64_t *indptr, const int32_t *indices,
   knn_grid(nq, n, &plen, &P);
   const dim3 g((unsigned)((nq + 255) / 256), (unsigned)P);
   k_radius_csr<0><<<g, NB, 0, s>>>(indptr, indices, data, q0, nq, n, eps,
-                                   plen, (unsigned long long *)counts,
-                                   nullptr, nullptr);
+                                   plen, out_f32 ? 1 : 0,
+                                   (unsigned long long *)counts, nullptr,
+                                   nullptr);
   return check_launch("radius csr count");
 }
 
 int dkm_radius_fill_csr_f64(const int64_t *indptr, const int32_t *indices,
                             const double *data, int64_t n, int64_t d,
-                            int64_t q0, int64_t nq, double eps,
+                            int64_t q0, int64_t nq, double eps, int out_f32,
                             const int64_t *offsets, void *ws, size_t ws_bytes,
                             int64_t *out_idx, double *out_dist,
                             void *stream) {
@@ -884,7 +907,8 @@ int dkm_radius_fill_csr_f64(const int64_t *indptr, const int32_t *indices,
   knn_grid(nq, n, &plen, &P);
   const dim3 g((unsigned)((nq + 255) / 256), (unsigned)P);
   k_radius_csr<1><<<g, NB, 0, s>>>(indptr, indices, data, q0, nq, n, eps,
-                                   plen, cur, out_idx, out_dist);
+                                   plen, out_f32 ? 1 : 0, cur, out_idx,
+                                   out_dist);
   if (int e = check_launch("radius csr fill")) return e;
   k_seg_sort<<<(unsigned)nq, NB, 0, s>>>(offsets, nq, out_idx, out_dist, sidx,
                                          sdist);

@@ -129,18 +129,25 @@ class NearestNeighbors:
             q = f if same else _csr_to(xq, dev)
             out_d = t.empty((nq, n_neighbors), dtype=t.float64, device=dev)
             out_i = t.empty((nq, n_neighbors), dtype=t.int64, device=dev)
+            # float32 on both sides: sklearn's upcast path (r rounded to
+            # float32, float32 sqrt)
+            f32 = 1 if (getattr(xf, "dkm_f32", False) and
+                        getattr(xq, "dkm_f32", False)) else 0
             if nq:
                 wsb = int(so.dkm_knn_workspace_bytes(nq, nx, n_neighbors))
                 ws = t.empty(max(wsb, 1), dtype=t.uint8, device=dev)
                 _lib.check(so.dkm_knn_csr_f64(
                     ptr(q[0]), ptr(q[1]), ptr(q[2]), nq, ptr(f[0]),
-                    ptr(f[1]), ptr(f[2]), nx, d, n_neighbors,
+                    ptr(f[1]), ptr(f[2]), nx, d, n_neighbors, f32,
                     ctypes.c_void_p(ws.data_ptr()), wsb, ptr(out_d),
                     ptr(out_i), stream_ptr()), "dkm_knn_csr_f64")
             ind = out_i.cpu().numpy()
             if not return_distance:
                 return ind
-            return out_d.cpu().numpy(), ind
+            dist = out_d.cpu().numpy()
+            # float32 Subsets: sklearn returns float32 distances (the
+            # values are float32 already)
+            return (dist.astype(np.float32) if f32 else dist), ind
 
 
 def _csr_to(m, dev):

@@ -354,11 +354,13 @@ int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
  * arithmetic of dkm_radius_count_csr_f64; neighbours ascending (r, index),
  * out_dist = sqrt(r).  kn in [1, nx] (passes of 32 beyond 32); workspace =
  * dkm_knn_workspace_bytes(nq, nx, kn).  The query and fit matrices may be
- * the same arrays. */
+ * the same arrays.  out_f32 != 0: the Subsets were float32 (data passed
+ * upcast to fp64): sklearn's upcast path rounds r to float32 before the
+ * max, ranks by it and takes the float32 sqrt; so do these. */
 int dkm_knn_csr_f64(const int64_t *q_indptr, const int32_t *q_indices,
                     const double *q_data, int64_t nq, const int64_t *x_indptr,
                     const int32_t *x_indices, const double *x_data,
-                    int64_t nx, int64_t d, int64_t kn, void *ws,
+                    int64_t nx, int64_t d, int64_t kn, int out_f32, void *ws,
                     size_t ws_bytes, double *out_dist, int64_t *out_idx,
                     void *stream);
 
@@ -387,14 +389,17 @@ int dkm_radius_fill_f64(const double *Q, int64_t nq, int64_t ldq,
  * n rows.  Distance = sklearn 1.7 euclidean_distances for fp64 CSR:
  * sqrt(max(((-2 q.x) + ||q||^2) + ||x||^2, 0)), row norms summed in stored
  * order, q.x by scipy csr_matmat order (increasing column of the
- * intersection).  Same two steps, offsets and workspace as the dense pair. */
+ * intersection).  Same two steps, offsets and workspace as the dense pair.
+ * out_f32 != 0 (float32 Subsets, data passed upcast to fp64): r rounded to
+ * float32, then max, the float32 sqrt and `dist < float32(eps)`, as
+ * sklearn's upcast path and numpy's float32 comparison do. */
 int dkm_radius_count_csr_f64(const int64_t *indptr, const int32_t *indices,
                              const double *data, int64_t n, int64_t d,
-                             int64_t q0, int64_t nq, double eps,
+                             int64_t q0, int64_t nq, double eps, int out_f32,
                              int64_t *counts, void *stream);
 int dkm_radius_fill_csr_f64(const int64_t *indptr, const int32_t *indices,
                             const double *data, int64_t n, int64_t d,
-                            int64_t q0, int64_t nq, double eps,
+                            int64_t q0, int64_t nq, double eps, int out_f32,
                             const int64_t *offsets, void *ws, size_t ws_bytes,
                             int64_t *out_idx, double *out_dist, void *stream);
 

@@ -196,14 +196,17 @@ def csr_sq_distances_to(qi, qv, indptr, indices, data, yy=None):
     return np.maximum(r, 0.0)
 
 
-def kneighbors_csr(f_csr, q_csr, n_neighbors):
+def kneighbors_csr(f_csr, q_csr, n_neighbors, f32=False):
     """Sparse ``kneighbors`` (reference neighbors/base.py:40-111 on CSR
     Subsets): sklearn fits brute force on CSR and ranks by
     ``pairwise_distances_chunked(squared=True)`` -- the squared distances of
     :func:`csr_sq_distances_to` -- then reports ``sqrt``.  ``f_csr`` /
     ``q_csr`` = (indptr, indices, data) with sorted indices.  Returns
     ``(dist, ind)`` ascending by (squared distance, fit row); the
-    reference's argpartition / argsort order equal distances arbitrarily."""
+    reference's argpartition / argsort order equal distances arbitrarily.
+    ``f32``: float32 Subsets -- sklearn's ``_euclidean_distances_upcast``
+    computes the same fp64 squares, casts them to float32, then max and
+    sqrt in float32."""
     fp, fi, fd = (np.asarray(a) for a in f_csr)
     qp, qi, qd = (np.asarray(a) for a in q_csr)
     fd = fd.astype(np.float64)
@@ -216,6 +219,8 @@ def kneighbors_csr(f_csr, q_csr, n_neighbors):
         a, b = qp[q], qp[q + 1]
         r = csr_sq_distances_to(qi[a:b], qd[a:b].astype(np.float64), fp, fi,
                                 fd, yy)
+        if f32:
+            r = r.astype(np.float32)
         o = np.lexsort((rows, r))[:n_neighbors]
         dist[q] = np.sqrt(r[o])
         ind[q] = o
@@ -223,13 +228,17 @@ def kneighbors_csr(f_csr, q_csr, n_neighbors):
 
 
 def compute_neighbours_csr(epsilon, min_samples, begin_idx, end_idx,
-                           indptr, indices, data):
+                           indptr, indices, data, f32=False):
     """Sparse ``_compute_neighbours``: same lists and flags as the dense
-    form, distances by :func:`csr_sq_distances` then ``sqrt``."""
+    form, distances by :func:`csr_sq_distances` then ``sqrt``.  ``f32``:
+    float32 Subsets (the squares cast to float32, float32 sqrt, and numpy
+    compares ``dist < epsilon`` in float32)."""
     n = len(indptr) - 1
     neighbour_list, core_points = [], []
+    data = np.asarray(data, np.float64)
     for q in range(*slice(begin_idx, end_idx).indices(n)):
-        dist = np.sqrt(csr_sq_distances(indptr, indices, data, q))
+        r = csr_sq_distances(indptr, indices, data, q)
+        dist = np.sqrt(r.astype(np.float32) if f32 else r)
         neigh = np.where(dist < epsilon)[0]
         neigh = neigh[np.lexsort((neigh, dist[neigh]))]
         neighbour_list.append(neigh)

@@ -50,6 +50,7 @@ DB_SPARSE_CASES = [
     ("dbs_wide", 300, 2000, 100, 0.005, 2.3, 2, 20, 280),   # ~10 nnz / row
     ("dbs_empty", 150, 30, 50, 0.03, 0.3, 2, 0, 150),       # empty rows
     ("dbs_blobs", 240, 20, 60, None, 5.5, 4, 30, 210),      # thresholded blobs
+    ("dbs_f32", 250, 40, 50, 0.15, 1.1, 3, 0, 250),         # float32 Subsets
 ]
 # sparse kneighbors (sklearn brute force on CSR):
 # (name, n_fit, n_query or None (query = fit), d, subset, density, n_neighbors)
@@ -59,6 +60,7 @@ KNN_SPARSE_CASES = [
     ("kns_empty", 150, None, 30, 50, 0.03, 4),      # empty rows: ties at 0
     ("kns_other", 240, 120, 20, 60, None, 6),       # queries != fit data
     ("kns_40", 400, None, 30, 100, 0.2, 40),        # > 32: two passes
+    ("kns_f32", 300, None, 40, 100, 0.15, 6),       # float32 Subsets
 ]
 
 
@@ -117,6 +119,8 @@ def generate():
         else:
             x = sp.random(n, d, density=dens, format="csr", random_state=rng,
                           data_rvs=lambda k: rng.uniform(-1, 1, k))
+        if name.endswith("_f32"):
+            x = x.astype(np.float32)
         x.sort_indices()
         ds = load_data(x, subset_size=sub)
         nl, cp = _compute_neighbours(eps, ms, True, b, e, *list(ds))
@@ -144,6 +148,8 @@ def generate():
                 x = sp.random(n, d, density=dens, format="csr",
                               random_state=rng,
                               data_rvs=lambda k: rng.uniform(-1, 1, k))
+            if name.endswith("_f32"):
+                x = x.astype(np.float32)
             x.sort_indices()
             return x
         xf = _csr(nf)

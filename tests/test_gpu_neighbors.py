@@ -272,9 +272,11 @@ def test_sparse_kneighbors_reference_golden(name):
     same = np.array_equal(f[0], q[0]) and np.array_equal(f[2], q[2]) and \
         np.array_equal(f[1], q[1])
     gd, gi = _knn_csr(mf, mq, sub, kn, same=same)
-    assert gi.dtype == np.int64 and gd.dtype == np.float64
+    assert gi.dtype == np.int64
     assert_knn_same_up_to_ties(gd, gi, dist, ind, name)
-    od, oi = orc.kneighbors_csr(f, q, kn)
+    f32 = f[2].dtype == np.float32
+    assert gd.dtype == (np.float32 if f32 else np.float64)
+    od, oi = orc.kneighbors_csr(f, q, kn, f32=f32)
     assert np.array_equal(gi, oi) and np.array_equal(gd, od)
 
 

@@ -85,7 +85,8 @@ def sparse_case(name):
 def test_oracle_sparse_epsilon_query_is_the_reference(name):
     ip, ix, dv, shape, meta, off, ref, core = sparse_case(name)
     sub, eps, ms, b, e = meta
-    nl, cp = orc.compute_neighbours_csr(eps, ms, int(b), int(e), ip, ix, dv)
+    nl, cp = orc.compute_neighbours_csr(eps, ms, int(b), int(e), ip, ix, dv,
+                                        f32=dv.dtype == np.float32)
     assert len(nl) == len(off) - 1
     for r, v in enumerate(nl):
         assert_same_up_to_ties(v, ref[off[r]:off[r + 1]], ip, ix, dv,
@@ -99,7 +100,8 @@ def assert_same_up_to_ties(v, w, ip, ix, dv, q, what):
     keys by index (dbs_empty: empty rows, all at distance 0)."""
     if np.array_equal(v, w):
         return
-    dist = np.sqrt(orc.csr_sq_distances(ip, ix, dv, q))
+    r = orc.csr_sq_distances(ip, ix, dv, q)
+    dist = np.sqrt(r.astype(np.float32) if dv.dtype == np.float32 else r)
     assert np.array_equal(np.sort(v), np.sort(w)), what
     assert np.array_equal(dist[v], dist[w]), what
 
@@ -114,7 +116,12 @@ def test_oracle_sparse_distances_are_sklearns_expansion():
         m = sp.csr_matrix((dv, ix, ip), shape=tuple(shape))
         for q in (0, 7, int(shape[0]) - 1):
             want = sk.pairwise_distances(m[q], m).ravel()
-            got = np.sqrt(orc.csr_sq_distances(ip, ix, dv, q))
+            r = orc.csr_sq_distances(ip, ix, dv, q)
+            # float32 Subsets: sklearn's upcast path (fp64 squares cast to
+            # float32, float32 sqrt)
+            got = np.sqrt(r.astype(np.float32) if dv.dtype == np.float32
+                          else r)
+            assert got.dtype == want.dtype, name
             assert np.array_equal(got, want), (name, q)
 
 
@@ -147,14 +154,17 @@ def assert_knn_same_up_to_ties(dist, ind, rdist, rind, what):
 @pytest.mark.parametrize("name", KNS)
 def test_oracle_sparse_kneighbors_is_the_reference(name):
     f, q, d, sub, kn, dist, ind = sparse_knn_case(name)
-    got_d, got_i = orc.kneighbors_csr(f, q, kn)
+    got_d, got_i = orc.kneighbors_csr(f, q, kn,
+                                      f32=f[2].dtype == np.float32)
     assert_knn_same_up_to_ties(got_d, got_i, dist, ind, name)
     # the indices name rows at the reported distances
     fm = sp_matrix(f, d)
     qm = sp_matrix(q, d)
     for r in (0, qm.shape[0] // 2, qm.shape[0] - 1):
-        want = np.sqrt(orc.csr_sq_distances_to(
-            qm[r].indices, qm[r].data, *f))
+        rr = orc.csr_sq_distances_to(qm[r].indices,
+                                     qm[r].data.astype(np.float64), *f)
+        want = np.sqrt(rr.astype(np.float32) if f[2].dtype == np.float32
+                       else rr)
         assert np.array_equal(want[ind[r]], dist[r]), (name, r)
     del fm
 
