@@ -312,11 +312,13 @@ def sorted_image_ok(dd, k):
             _lib.IMAGE_SINGLE and bool(so.dkm_x_image_sorted_ok(int(k), dd.d)))
 
 
-def sorted_image(dd, labels, k, ws, old=None):
+def sorted_image(dd, labels, k, ws, old=None, acc=None):
     """dkm_x_image_sorted_*: the sample image with its rows grouped by
     ``labels`` (a fit's current assignment), as (tensor, IMAGE_SORTED); the
     buffer of ``old`` is reused.  (None, 0) when it would leave less than
-    4 GiB of HBM free or the workspace's label scratch is shorter than n.
+    4 GiB of HBM free or the workspace's label scratch is shorter than n
+    (then ``acc`` is untouched).  With ``acc``: also acc += the [sums |
+    counts] of X by ``labels`` (dkm_x_image_sorted_sums_*, one pass over X).
     The image carries a copy of the labels: pass it to every later call
     that updates them (partial_sum / assign_delta ``image=``)."""
     t = torch()
@@ -331,8 +333,15 @@ def sorted_image(dd, labels, k, ws, old=None):
         img = t.empty(nb, dtype=t.uint8, device=dd.device)
     if int(so.dkm_workspace_bytes(int(k), dd.d, dd.n)) > ws.nbytes:
         return None, 0
-    fn = so.dkm_x_image_sorted_f32 if dd.dtype == np.float32 else \
-        so.dkm_x_image_sorted_f64
+    f32 = dd.dtype == np.float32
+    if acc is not None:
+        fn = so.dkm_x_image_sorted_sums_f32 if f32 else \
+            so.dkm_x_image_sorted_sums_f64
+        _lib.check(fn(ptr(dd.X), dd.n, dd.d, dd.X.stride(0), ptr(labels),
+                      int(k), ws.p, ws.nbytes, ptr(img), nb, ptr(acc),
+                      stream_ptr()), "dkm_x_image_sorted_sums")
+        return img, _lib.IMAGE_SORTED
+    fn = so.dkm_x_image_sorted_f32 if f32 else so.dkm_x_image_sorted_f64
     _lib.check(fn(ptr(dd.X), dd.n, dd.d, dd.X.stride(0), ptr(labels), int(k),
                   ws.p, ws.nbytes, ptr(img), nb, stream_ptr()),
                "dkm_x_image_sorted")

@@ -49,6 +49,10 @@ SIGNATURES = {
                                       _sz, _p, _sz, _p]),
     "dkm_x_image_sorted_f32": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p,
                                       _sz, _p, _sz, _p]),
+    "dkm_x_image_sorted_sums_f64": (_i32, [_p, _i64, _i64, _i64, _p, _i64,
+                                           _p, _sz, _p, _sz, _p, _p]),
+    "dkm_x_image_sorted_sums_f32": (_i32, [_p, _i64, _i64, _i64, _p, _i64,
+                                           _p, _sz, _p, _sz, _p, _p]),
     "dkm_partial_sum_img_f64": (_i32, [_p, _p, _i32, _sz, _i64, _i64, _i64,
                                        _p, _i64, _p, _sz, _p, _p, _i32, _p]),
     "dkm_partial_sum_img_f32": (_i32, [_p, _p, _i32, _sz, _i64, _i64, _i64,

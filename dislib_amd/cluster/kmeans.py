@@ -165,6 +165,9 @@ REFRESH = int(os.environ.get("DKM_REFRESH", "64"))
 # (DKM_SORTED_IMAGE=0: A/B and parity runs).
 SORTED_IMAGE = os.environ.get("DKM_SORTED_IMAGE", "1") != "0"
 SORT_AT = 1
+# build the sorted image and iteration SORT_AT's sums in one pass over X
+# (dkm_x_image_sorted_sums_*); "0": partial_sum, then the image (A/B runs)
+FUSED_SORT_SUMS = os.environ.get("DKM_FUSED_SORT_SUMS", "1") != "0"
 # A/B knobs of the first two iterations (auto mode): the screen of iteration
 # 0 against the initial centres ("bf16x3" or the single product "bf16"), and
 # whether iteration 1 uses iteration 0's labels as hints ("0": top-3 pass)
@@ -250,7 +253,8 @@ class _Lloyd:
         """The hot kernel: fused assignment over all resident samples, full
         partial sums (dkm_partial_sum_*) or incremental (dkm_assign_delta_*).
         """
-        from .._device import assign_delta, partial_sum, sorted_image
+        from .._device import (assign_delta, label_sums, partial_sum,
+                               predict, sorted_image)
         if self.dd.n == 0:
             return
         mode = self.mode
@@ -275,6 +279,18 @@ class _Lloyd:
             else:
                 image = self.simg or (None, 0)
         with self._on():
+            if self.sorting and self.it == SORT_AT and FUSED_SORT_SUMS:
+                # labels only, then the sorted image and this iteration's
+                # full sums in one pass over X (iteration 1 always recomputes
+                # in full: _full())
+                lab = self.labels[:self.dd.n]
+                predict(self.dd, self.C, self.ws, lab, mode)
+                simg = sorted_image(self.dd, lab, self.k, self.ws,
+                                    acc=self.acc)
+                if simg[0] is None:
+                    label_sums(self.dd, self.ws, lab, self.acc, self.k)
+                self.simg = simg if simg[0] is not None else None
+                return
             if self._full():
                 partial_sum(self.dd, self.C, self.ws, self.labels, self.acc,
                             mode, image=image)

@@ -1172,6 +1172,105 @@ static int launch_image_tiles(const TX *X, int64_t n, int d, int64_t ldx,
   return check_launch("sample image");
 }
 
+// The label-sorted image AND the full sums in one pass over X (the fit's
+// first sorted iteration would otherwise read X once for the sums and once
+// for the image).  Block b takes a contiguous range of 32-row tiles of the
+// sorted order; a tile's rows are staged in LDS as fp64: the image tile and
+// |x|^2 come from them exactly as k_x_image writes them, and the sums from
+// the fp64 values, one running sum per (row group, feature) of the current
+// cluster (positions < m are labelled and ascending by label), added to acc
+// with fp64 atomics when the cluster changes and at the end of the range.
+template <class TX, int NKS>
+__global__ void __launch_bounds__(256)
+    k_x_image_sums(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
+                   const int32_t *__restrict__ perm,
+                   const int32_t *__restrict__ off, int k,
+                   uint16_t *__restrict__ tiles, float *__restrict__ xx,
+                   double *__restrict__ acc) {
+  constexpr int DP = 16 * NKS, LD = DP + 1, RG = 256 / DP;
+  static_assert(256 % DP == 0, "DP divides the block");
+  __shared__ double s[32 * LD];
+  __shared__ int64_t srow[32];
+  const int64_t nt = (n + 31) / 32;
+  const int64_t per = (nt + gridDim.x - 1) / gridDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * per;
+  const int64_t t1 = t0 + per < nt ? t0 + per : nt;
+  if (t0 >= t1) return;
+  const int64_t m = off[k];  // labelled positions
+  const int f = threadIdx.x % DP, g = threadIdx.x / DP;
+  // the cluster of the range's first position: largest c, off[c] <= p
+  int c = 0;
+  {
+    const int64_t p0 = t0 * 32;
+    int lo = 0, hi = k;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (off[mid] <= p0) lo = mid;
+      else hi = mid;
+    }
+    c = lo;
+  }
+  int64_t nxt = off[c + 1];
+  double a = 0.0;
+  int cnt = 0;
+  auto flush = [&]() {
+    if (cnt) {
+      if (f < d) atomic_add_f64(acc + (int64_t)c * d + f, a);
+      if (f == 0) atomic_add_f64(acc + (int64_t)k * d + c, (double)cnt);
+    }
+    a = 0.0;
+    cnt = 0;
+  };
+  for (int64_t t = t0; t < t1; ++t) {
+    const int64_t r0 = t * 32;
+    __syncthreads();  // the previous tile's reads are done
+    if (threadIdx.x < 32) srow[threadIdx.x] = (int64_t)perm[r0 + threadIdx.x];
+    __syncthreads();
+    for (int e = threadIdx.x; e < 32 * DP; e += 256) {
+      const int row = e / DP, col = e % DP;
+      const int64_t src = srow[row];
+      double v = 0.0;
+      if (src >= 0 && col < d) v = (double)X[src * ldx + col];
+      s[row * LD + col] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {  // |x|^2 as k_x_image: fp64 fma of the fp32s
+      double q = 0.0;
+      for (int col = 0; col < DP; ++col) {
+        const double v = (double)(float)s[threadIdx.x * LD + col];
+        q = fma(v, v, q);
+      }
+      xx[r0 + threadIdx.x] = (float)q;
+    }
+    for (int e = threadIdx.x; e < NKS * 64; e += 256) {
+      const int ks = e >> 6, l = e & 63;
+      const double *src = s + (l & 31) * LD + 16 * ks + 8 * (l >> 5);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const bf16x2 b = __builtin_convertvector(
+            f32x2{(float)src[j], (float)src[j + 1]}, bf16x2);
+        o[j] = b[0];
+        o[j + 1] = b[1];
+      }
+      *((bf16x8 *)(tiles + t * (NKS * 512)) + e) = o;
+    }
+    // sums: row group g takes rows g, g + RG, ... of the tile
+    for (int r = g; r < 32; r += RG) {
+      const int64_t p = r0 + r;
+      if (p >= m) break;  // unlabelled / padding rows: no sums
+      if (p >= nxt) {
+        flush();
+        while (off[c + 1] <= p) ++c;
+        nxt = off[c + 1];
+      }
+      a += s[r * LD + f];
+      ++cnt;
+    }
+  }
+  flush();
+}
+
 template <class TX>
 int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, int kind,
                    void *image, int cus, hipStream_t s) {
@@ -1249,7 +1348,7 @@ static unsigned flat_grid(int64_t n, int cus) {
 template <class TX>
 int launch_x_image_sorted(const TX *X, int64_t n, int d, int64_t ldx,
                           const int32_t *labels, int k, const WsView &v,
-                          void *image, int cus, hipStream_t s) {
+                          void *image, int cus, hipStream_t s, double *acc) {
   const XImage im = x_image_view(image, n, d, IMG_SORTED);
   const int64_t ntot = (n + 31) / 32 * 32;
   int32_t *perm = (int32_t *)im.perm;
@@ -1262,17 +1361,35 @@ int launch_x_image_sorted(const TX *X, int64_t n, int d, int64_t ldx,
   k_perm_unlabelled<<<g, 256, 0, s>>>(labels, n, k, v.soff + k, cnt, perm);
   k_plab<<<g, 256, 0, s>>>(perm, labels, ntot, im.plab, 0);
   if (int r = check_launch("sorted image: permutation")) return r;
-  return launch_image_tiles<TX>(X, n, d, ldx, perm, im, cus, s);
+  if (!acc) return launch_image_tiles<TX>(X, n, d, ldx, perm, im, cus, s);
+  const int64_t nt = (n + 31) / 32;
+  const unsigned gs =
+      (unsigned)std::max<int64_t>(1, std::min<int64_t>(nt, (int64_t)cus * 8));
+  uint16_t *tiles = (uint16_t *)im.tiles;
+  float *xx = (float *)im.xx;
+  switch ((int)(dpad16(d) / 16)) {
+#define DKM_XS(N)                                                           \
+  case N:                                                                   \
+    k_x_image_sums<TX, N><<<gs, 256, 0, s>>>(X, n, d, ldx, perm, v.soff, k, \
+                                             tiles, xx, acc);               \
+    break;
+    DKM_XS(1) DKM_XS(2) DKM_XS(4) DKM_XS(8)
+#undef DKM_XS
+    default:  // the caller checks x_image_sums_fused(d)
+      return fail(DKM_E_ARG, "sorted image + sums: dpad16(d) / 16 not 1, 2, "
+                             "4 or 8");
+  }
+  return check_launch("sorted image + sums");
 }
 
 template int launch_x_image_sorted<double>(const double *, int64_t, int,
                                            int64_t, const int32_t *, int,
                                            const WsView &, void *, int,
-                                           hipStream_t);
+                                           hipStream_t, double *);
 template int launch_x_image_sorted<float>(const float *, int64_t, int,
                                           int64_t, const int32_t *, int,
                                           const WsView &, void *, int,
-                                          hipStream_t);
+                                          hipStream_t, double *);
 
 int launch_plab_sync(const XImage &img, int64_t n, const int32_t *lab,
                      int cus, hipStream_t s) {

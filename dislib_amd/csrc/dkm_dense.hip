@@ -2912,6 +2912,16 @@ static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
   return 0;
 }
 
+// A/B knob (DKM_AB_AUTO_SINGLE=1): AUTO picks the single-product screen
+// also where the fp64 sums fit LDS beside the bf16x3 fragments (C2)
+static bool ab_auto_single() {
+  static const bool v = [] {
+    const char *e = getenv("DKM_AB_AUTO_SINGLE");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 template <class TX>
 static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                   const double *C, int64_t k, const void *ws, size_t wsb,
@@ -2936,7 +2946,8 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
            // the GEMM screen (d > 128) and sums beyond LDS with the bf16
            // centres resident: the single product
            : gemm_path(k, d) ||
-                   (screen_ok(k, d) && b1_ok(k, d) && !sums_fit_lds(k, d))
+                   (screen_ok(k, d) && b1_ok(k, d) &&
+                    (!sums_fit_lds(k, d) || ab_auto_single()))
                ? DKM_MODE_SCREEN_BF16
                : DKM_MODE_SCREEN_BF16X3;
   if (image && (image_kind < IMG_SINGLE || image_kind > IMG_GEMM ||
@@ -3012,7 +3023,7 @@ template <class TX>
 static int x_image_sorted(const TX *X, int64_t n, int64_t d, int64_t ldx,
                           const int32_t *labels, int64_t k, const void *ws,
                           size_t wsb, void *image, size_t image_bytes,
-                          void *stream, const char *who) {
+                          double *acc, void *stream, const char *who) {
   const std::string w(who);
   if (n < 0 || d <= 0 || ldx < d || k <= 1 || k > INT32_MAX)
     return fail(DKM_E_ARG, w + ": bad n/d/k/ldx");
@@ -3027,8 +3038,16 @@ static int x_image_sorted(const TX *X, int64_t n, int64_t d, int64_t ldx,
   if (int r = ws_view(ws, wsb, k, d, &v)) return r;
   if (!sorted_sums_ok(k, n, v))
     return fail(DKM_E_WORKSPACE, w + ": workspace label scratch < n");
-  return launch_x_image_sorted<TX>(X, n, (int)d, ldx, labels, (int)k, v, image,
-                                   dev_info().cus, (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  const bool fused = acc && x_image_sums_fused(d);
+  if (int r = launch_x_image_sorted<TX>(X, n, (int)d, ldx, labels, (int)k, v,
+                                        image, dev_info().cus, s,
+                                        fused ? acc : nullptr))
+    return r;
+  if (acc && !fused)
+    return launch_post_sums<TX>(X, 0, n, (int)d, ldx, labels, nullptr,
+                                (int)k, acc, v, s);
+  return 0;
 }
 
 template <class TX>
@@ -3113,7 +3132,8 @@ int dkm_x_image_kind(int64_t k, int64_t d, int mode) {
                                                                  : IMG_NONE;
   if (d > 128 || !screen_ok(k, d)) return IMG_NONE;
   if (mode == DKM_MODE_AUTO)
-    mode = b1_ok(k, d) && !sums_fit_lds(k, d) ? DKM_MODE_SCREEN_BF16
+    mode = b1_ok(k, d) && (!sums_fit_lds(k, d) || ab_auto_single())
+               ? DKM_MODE_SCREEN_BF16
                                               : DKM_MODE_SCREEN_BF16X3;
   if (mode == DKM_MODE_SCREEN_BF16)
     return b1_ok(k, d) && b2_lds_bytes(k, d) <= 160 * 1024
@@ -3161,7 +3181,8 @@ int dkm_x_image_sorted_f64(const double *X, int64_t n, int64_t d, int64_t ldx,
                            size_t ws_bytes, void *image, size_t image_bytes,
                            void *stream) {
   return x_image_sorted<double>(X, n, d, ldx, labels, k, ws, ws_bytes, image,
-                                image_bytes, stream, "dkm_x_image_sorted_f64");
+                                image_bytes, nullptr, stream,
+                                "dkm_x_image_sorted_f64");
 }
 
 int dkm_x_image_sorted_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
@@ -3169,7 +3190,30 @@ int dkm_x_image_sorted_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
                            size_t ws_bytes, void *image, size_t image_bytes,
                            void *stream) {
   return x_image_sorted<float>(X, n, d, ldx, labels, k, ws, ws_bytes, image,
-                               image_bytes, stream, "dkm_x_image_sorted_f32");
+                               image_bytes, nullptr, stream,
+                               "dkm_x_image_sorted_f32");
+}
+
+int dkm_x_image_sorted_sums_f64(const double *X, int64_t n, int64_t d,
+                                int64_t ldx, const int32_t *labels, int64_t k,
+                                const void *ws, size_t ws_bytes, void *image,
+                                size_t image_bytes, double *acc,
+                                void *stream) {
+  if (!acc) return fail(DKM_E_ARG, "x_image_sorted_sums: acc is NULL");
+  return x_image_sorted<double>(X, n, d, ldx, labels, k, ws, ws_bytes, image,
+                                image_bytes, acc, stream,
+                                "dkm_x_image_sorted_sums_f64");
+}
+
+int dkm_x_image_sorted_sums_f32(const float *X, int64_t n, int64_t d,
+                                int64_t ldx, const int32_t *labels, int64_t k,
+                                const void *ws, size_t ws_bytes, void *image,
+                                size_t image_bytes, double *acc,
+                                void *stream) {
+  if (!acc) return fail(DKM_E_ARG, "x_image_sorted_sums: acc is NULL");
+  return x_image_sorted<float>(X, n, d, ldx, labels, k, ws, ws_bytes, image,
+                               image_bytes, acc, stream,
+                               "dkm_x_image_sorted_sums_f32");
 }
 
 #define DKM_IMG_CHECK(who)                                                  \

@@ -190,10 +190,17 @@ XImage x_image_view(const void *image, int64_t n, int64_t d, int kind);
 template <class TX>
 int launch_x_image(const TX *X, int64_t n, int d, int64_t ldx, int kind,
                    void *image, int cus, hipStream_t s);
+// acc != NULL: also acc += the full [sums | counts] of X by labels, in the
+// same pass over X (x_image_sums_fused(d) must hold)
 template <class TX>
 int launch_x_image_sorted(const TX *X, int64_t n, int d, int64_t ldx,
                           const int32_t *labels, int k, const WsView &v,
-                          void *image, int cus, hipStream_t s);
+                          void *image, int cus, hipStream_t s,
+                          double *acc = nullptr);
+inline bool x_image_sums_fused(int64_t d) {
+  const int64_t nks = (d + 15) / 16;
+  return nks == 1 || nks == 2 || nks == 4 || nks == 8;
+}
 // IMG_SORTED: plab <- labels[perm] where the screen marked it (-1) for a
 // re-check kernel; no-op for the other kinds
 int launch_plab_sync(const XImage &img, int64_t n, const int32_t *lab,

@@ -173,6 +173,20 @@ int dkm_x_image_sorted_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
                            const int32_t *labels, int64_t k, const void *ws,
                            size_t ws_bytes, void *image, size_t image_bytes,
                            void *stream);
+/* The same image, and acc += the full [sums | counts] of X by `labels` (the
+ * dkm_label_sums_* result) in the same pass over X: a fit that builds the
+ * image from an iteration's labels gets that iteration's sums without a
+ * second read of X (predict, then this call, instead of partial_sum, then
+ * dkm_x_image_sorted_*).  Sums are fp64 atomics: equal to dkm_label_sums_*
+ * up to the order of the additions.                                        */
+int dkm_x_image_sorted_sums_f64(const double *X, int64_t n, int64_t d,
+                                int64_t ldx, const int32_t *labels, int64_t k,
+                                const void *ws, size_t ws_bytes, void *image,
+                                size_t image_bytes, double *acc, void *stream);
+int dkm_x_image_sorted_sums_f32(const float *X, int64_t n, int64_t d,
+                                int64_t ldx, const int32_t *labels, int64_t k,
+                                const void *ws, size_t ws_bytes, void *image,
+                                size_t image_bytes, double *acc, void *stream);
 /* image_bytes: the image buffer's size, checked against
  * dkm_x_image_bytes(n, d, image_kind) (an image built for other n or d is
  * refused instead of read out of bounds).                                 */

@@ -144,3 +144,43 @@ def test_sorted_and_unsorted_fits_agree(monkeypatch, seed, blobs, std):
     assert 0 < blocks <= 32 * tiles
     if blobs == 1000:       # separated blobs: most blocks are cleared
         assert blocks < 16 * tiles, (blocks, tiles)
+
+
+@pytest.mark.parametrize("n,d,k,f32", [(5000, 64, 300, False),
+                                       (4100, 128, 200, True),
+                                       (777, 16, 2000, False),
+                                       (3000, 40, 100, False),
+                                       (9000, 20, 64, True)])
+def test_sorted_image_sums_fused(n, d, k, f32):
+    """dkm_x_image_sorted_sums_*: the same image bytes as
+    dkm_x_image_sorted_*, and acc += the dkm_label_sums_* result (fp64
+    atomics: equal up to the order of the additions); d = 40 (three 16-wide
+    slices) takes the image, then the separate sums."""
+    from dislib_amd import _device, _lib
+    from dislib_amd.data import load_data
+    so = _lib.lib()
+    if not so.dkm_x_image_sorted_ok(k, d):
+        pytest.skip("(k, d) does not take the sorted image")
+    rng = np.random.default_rng(n + d + k)
+    x = rng.standard_normal((n, d)) * 10.0 ** rng.integers(-2, 3, (n, 1))
+    if f32:
+        x = x.astype(np.float32)
+    lab = rng.integers(0, k, n).astype(np.int32)
+    lab[: n // 3] = rng.integers(0, 3, n // 3)          # a few big clusters
+    dev = torch.device("cuda", 0)
+    dd = load_data(x, subset_size=n)._device_data()
+    ws = _device.Workspace(k, d, n, dev)
+    lt = torch.from_numpy(lab).to(dev)
+    img0, _ = _device.sorted_image(dd, lt, k, ws)
+    want = torch.full((k * (d + 1),), 0.5, dtype=torch.float64, device=dev)
+    _device.label_sums(dd, ws, lt, want, k)
+    acc = torch.full_like(want, 0.5)
+    img1, kind = _device.sorted_image(dd, lt, k, ws, acc=acc)
+    assert kind == _lib.IMAGE_SORTED
+    assert torch.equal(img0, img1)
+    a, w = acc.cpu().numpy(), want.cpu().numpy()      # [sums k x d | counts]
+    assert np.array_equal(a[k * d:], w[k * d:])
+    scale = np.zeros((k, d))
+    np.add.at(scale, lab, np.abs(x.astype(np.float64)))
+    assert np.all(np.abs(a[:k * d] - w[:k * d]) <=
+                  1e-13 * (scale.ravel() + 1.0))
