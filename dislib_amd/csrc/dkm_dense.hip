@@ -2912,16 +2912,6 @@ static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
   return 0;
 }
 
-// A/B knob (DKM_AB_AUTO_SINGLE=1): AUTO picks the single-product screen
-// also where the fp64 sums fit LDS beside the bf16x3 fragments (C2)
-static bool ab_auto_single() {
-  static const bool v = [] {
-    const char *e = getenv("DKM_AB_AUTO_SINGLE");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
 template <class TX>
 static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                   const double *C, int64_t k, const void *ws, size_t wsb,
@@ -2947,7 +2937,7 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
            // centres resident: the single product
            : gemm_path(k, d) ||
                    (screen_ok(k, d) && b1_ok(k, d) &&
-                    (!sums_fit_lds(k, d) || ab_auto_single()))
+                    !sums_fit_lds(k, d))
                ? DKM_MODE_SCREEN_BF16
                : DKM_MODE_SCREEN_BF16X3;
   if (image && (image_kind < IMG_SINGLE || image_kind > IMG_GEMM ||
@@ -3132,8 +3122,7 @@ int dkm_x_image_kind(int64_t k, int64_t d, int mode) {
                                                                  : IMG_NONE;
   if (d > 128 || !screen_ok(k, d)) return IMG_NONE;
   if (mode == DKM_MODE_AUTO)
-    mode = b1_ok(k, d) && (!sums_fit_lds(k, d) || ab_auto_single())
-               ? DKM_MODE_SCREEN_BF16
+    mode = b1_ok(k, d) && !sums_fit_lds(k, d) ? DKM_MODE_SCREEN_BF16
                                               : DKM_MODE_SCREEN_BF16X3;
   if (mode == DKM_MODE_SCREEN_BF16)
     return b1_ok(k, d) && b2_lds_bytes(k, d) <= 160 * 1024

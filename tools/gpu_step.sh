@@ -20,7 +20,6 @@ for s in "$@"; do
   case $s in
     t_new) step t_new 600 $PT tests/test_gpu_sorted.py tests/test_gpu_b2.py tests/test_gpu_nonfinite.py tests/test_gpu_fullsize.py ;;
     t_sorted) step t_sorted 300 $PT tests/test_gpu_sorted.py ;;
-    c2ab) step c2ab 1200 bash tools/gpu_c2ab.sh $TAG; cat $OUT/${TAG}_c2ab.log ;;
     c3fab) for r in 1 2; do for v in 0 1; do
         DKM_FUSED_SORT_SUMS=$v step c3f$v$r 300 python bench.py --n 125000000 --d 64 --k 1000 --steps 8 --warmup 2 --no-cpu --only-headline
         python -c "import json,sys;d=json.loads([l for l in open('$OUT/${TAG}_c3f$v$r.log') if l.startswith('{')][-1]);print('fused=$v', round(d['ms_per_step'],3), 'fit', round(d['fit_ms_per_iter'],2), d.get('fit_iters'))"
