@@ -66,6 +66,7 @@
 
 #include <algorithm>
 #include <string>
+#include <type_traits>
 
 #include "dkm_internal.h"
 
@@ -198,37 +199,47 @@ __global__ void __launch_bounds__(CSR_BLOCK)
           myi = indices[c0 + gl];
           myv = (float)data[c0 + gl];
         }
-        // the chunk's C^T row loads first, then the fmas
-        float4 cv[CSR_G][NP];
-        float vv[CSR_G];
+        // the chunk's C^T row loads first, then the fmas.  Lanes past the
+        // group's entries hold (0, 0.0): when every group of the wave has a
+        // full chunk, the loads and fmas run without masks (FULL); pass
+        // blocks past the slice are wave-uniform skips.
+        auto chunk = [&](auto full_tag) {
+          constexpr bool FULL = decltype(full_tag)::value;
+          float4 cv[CSR_G][NP];
+          float vv[CSR_G];
 #pragma unroll
-        for (int e = 0; e < CSR_G; ++e) {
-          const int idx = __shfl(myi, gbase + e, WAVE);
-          vv[e] = __shfl(myv, gbase + e, WAVE);
-          // element offset < 2^31: d x ks floats per slice
-          const float *row = CTs + (uint32_t)(idx * ks + jp + 4 * gl);
-#pragma unroll
-          for (int p = 0; p < NP; ++p) {
-            const int j = jp + CSR_PASS * p + 4 * gl;
-            cv[e][p] = (e < cnt && j < j_hi)
-                           ? *(const float4 *)(row + CSR_PASS * p)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < CSR_G; ++e) {
-          if (e < cnt) {
-            const float v = vv[e];
-            if (first) xx = fmaf(v, v, xx);
+          for (int e = 0; e < CSR_G; ++e) {
+            const int idx = __shfl(myi, gbase + e, WAVE);
+            vv[e] = __shfl(myv, gbase + e, WAVE);
+            // element offset < 2^31: d x ks floats per slice
+            const float *row = CTs + (uint32_t)(idx * ks + jp + 4 * gl);
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
-              dot[p][0] = fmaf(v, cv[e][p].x, dot[p][0]);
-              dot[p][1] = fmaf(v, cv[e][p].y, dot[p][1]);
-              dot[p][2] = fmaf(v, cv[e][p].z, dot[p][2]);
-              dot[p][3] = fmaf(v, cv[e][p].w, dot[p][3]);
+              const bool blk = p == 0 || jp + CSR_PASS * p < j_hi;
+              cv[e][p] = (blk && (FULL || e < cnt))
+                             ? *(const float4 *)(row + CSR_PASS * p)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
             }
           }
-        }
+#pragma unroll
+          for (int e = 0; e < CSR_G; ++e) {
+            if (FULL || e < cnt) {
+              const float v = vv[e];
+              if (first) xx = fmaf(v, v, xx);
+#pragma unroll
+              for (int p = 0; p < NP; ++p) {
+                dot[p][0] = fmaf(v, cv[e][p].x, dot[p][0]);
+                dot[p][1] = fmaf(v, cv[e][p].y, dot[p][1]);
+                dot[p][2] = fmaf(v, cv[e][p].z, dot[p][2]);
+                dot[p][3] = fmaf(v, cv[e][p].w, dot[p][3]);
+              }
+            }
+          }
+        };
+        if (__all(cnt == CSR_G))
+          chunk(std::true_type{});
+        else
+          chunk(std::false_type{});
       }
 #pragma unroll
       for (int p = 0; p < NP; ++p) {

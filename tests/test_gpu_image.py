@@ -97,9 +97,12 @@ def test_w32_delta_through_the_image(monkeypatch, image, d, k):
     assert err <= 1e-11
 
 
-def test_c2_shape_reads_the_split_image():
+def test_image_kind_per_config():
+    """C2 reads the split image, C3 the single one, C4 the GEMM tiles
+    (round 4); the exact mode takes none."""
     from dislib_amd import _lib
     so = _lib.lib()
     assert so.dkm_x_image_kind(100, 32, _lib.MODE_AUTO) == _lib.IMAGE_SPLIT
     assert so.dkm_x_image_kind(1000, 64, _lib.MODE_AUTO) == _lib.IMAGE_SINGLE
-    assert so.dkm_x_image_kind(4096, 1024, _lib.MODE_AUTO) == _lib.IMAGE_NONE
+    assert so.dkm_x_image_kind(4096, 1024, _lib.MODE_AUTO) == _lib.IMAGE_GEMM
+    assert so.dkm_x_image_kind(4096, 1024, _lib.MODE_EXACT) == _lib.IMAGE_NONE
