@@ -199,16 +199,18 @@ __global__ void __launch_bounds__(CSR_BLOCK)
           myi = indices[c0 + gl];
           myv = (float)data[c0 + gl];
         }
-        // the chunk's C^T row loads first, then the fmas.  Lanes past the
-        // group's entries hold (0, 0.0): when every group of the wave has a
-        // full chunk, the loads and fmas run without masks (FULL); pass
-        // blocks past the slice are wave-uniform skips.
-        auto chunk = [&](auto full_tag) {
-          constexpr bool FULL = decltype(full_tag)::value;
-          float4 cv[CSR_G][NP];
-          float vv[CSR_G];
+        // the chunk's C^T row loads first, then the fmas, over the first E
+        // entries (E = 8, or 2 when no group of the wave has more left):
+        // lanes past a group's entries hold (0, 0.0), so a shorter group's
+        // extra entries load row 0 and add +-0 (a non-finite centre value
+        // leaves every sample undecided anyway, through B).  No exec masks;
+        // pass blocks past the slice are wave-uniform skips.
+        auto chunk = [&](auto e_tag) {
+          constexpr int E = decltype(e_tag)::value;
+          float4 cv[E][NP];
+          float vv[E];
 #pragma unroll
-          for (int e = 0; e < CSR_G; ++e) {
+          for (int e = 0; e < E; ++e) {
             const int idx = __shfl(myi, gbase + e, WAVE);
             vv[e] = __shfl(myv, gbase + e, WAVE);
             // element offset < 2^31: d x ks floats per slice
@@ -216,30 +218,27 @@ __global__ void __launch_bounds__(CSR_BLOCK)
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
               const bool blk = p == 0 || jp + CSR_PASS * p < j_hi;
-              cv[e][p] = (blk && (FULL || e < cnt))
-                             ? *(const float4 *)(row + CSR_PASS * p)
+              cv[e][p] = blk ? *(const float4 *)(row + CSR_PASS * p)
                              : make_float4(0.f, 0.f, 0.f, 0.f);
             }
           }
 #pragma unroll
-          for (int e = 0; e < CSR_G; ++e) {
-            if (FULL || e < cnt) {
-              const float v = vv[e];
-              if (first) xx = fmaf(v, v, xx);
+          for (int e = 0; e < E; ++e) {
+            const float v = vv[e];
+            if (first) xx = fmaf(v, v, xx);
 #pragma unroll
-              for (int p = 0; p < NP; ++p) {
-                dot[p][0] = fmaf(v, cv[e][p].x, dot[p][0]);
-                dot[p][1] = fmaf(v, cv[e][p].y, dot[p][1]);
-                dot[p][2] = fmaf(v, cv[e][p].z, dot[p][2]);
-                dot[p][3] = fmaf(v, cv[e][p].w, dot[p][3]);
-              }
+            for (int p = 0; p < NP; ++p) {
+              dot[p][0] = fmaf(v, cv[e][p].x, dot[p][0]);
+              dot[p][1] = fmaf(v, cv[e][p].y, dot[p][1]);
+              dot[p][2] = fmaf(v, cv[e][p].z, dot[p][2]);
+              dot[p][3] = fmaf(v, cv[e][p].w, dot[p][3]);
             }
           }
         };
-        if (__all(cnt == CSR_G))
-          chunk(std::true_type{});
+        if (__any(cnt > 2))
+          chunk(std::integral_constant<int, 8>{});
         else
-          chunk(std::false_type{});
+          chunk(std::integral_constant<int, 2>{});
       }
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
