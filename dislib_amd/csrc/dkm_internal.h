@@ -237,7 +237,9 @@ constexpr int TL_SEGS = 8192;
 // so that the lines of a slice spread over every set of an XCD's L2 (rows
 // of the full d x k transpose, 1 KB apart at k = 256, fell into one set in
 // eight: 10 % L2 misses at C5, profiles/r04/pmc/c5_csr_pmc_summary_4M.txt).
-constexpr size_t CSR_SLICE_BYTES = 2u << 20;
+// 16 MB: every slice costs a walk over the entries, which outweighs the L2
+// locality of smaller slices (C5's 10 MB table: one slice is fastest).
+constexpr size_t CSR_SLICE_BYTES = 16u << 20;
 constexpr int CSR_PASS = 32;
 __host__ __device__ inline int csr_slices(int64_t k, int64_t d) {
   int S = 1;

@@ -16,11 +16,14 @@
 // reference arithmetic picks the same centre, otherwise by that arithmetic.
 //
 // The time goes into gathering nnz rows of C^T per sample (k values each:
-// 10 KB in fp32 at C5, k = 256, 10 nnz) from a table no L2 holds whole.
-// So the centres are cut into S slices (S = 1, 2, 4 or 8) small enough for
-// one XCD's 4 MB L2, and block b works on slice b % S: blocks b and b + 8
-// share an XCD, so each XCD gathers from its own slice only (a speed
-// assumption, never a correctness one).
+// 10 KB in fp32 at C5, k = 256, 10 nnz).  Large tables are cut into S
+// slices (S = 1, 2, 4 or 8; CSR_SLICE_BYTES) and block b works on slice
+// b % S, so blocks b and b + 8 share an XCD and gather from one slice (a
+// speed assumption, never a correctness one).  Every slice costs a walk
+// over the sample's entries, a reduction and a state per sample, and that
+// costs more than the L2 locality gains: at C5 the 10 MB table runs as ONE
+// slice (S = 1: 7.0 ms per step; S = 2: 7.3, S = 4: 7.6, S = 8 (4 MB-L2
+// slices): 8.8; profiles/r04/c5ab).
 //   k_csr_screen   8 lanes per sample (8 samples per wave), 4 centres per
 //                  lane per 32-centre pass, 16-B loads of the fp32 C^T
 //                  (d x ct_ld(k)); the row's entries staged 8 at a time in
@@ -199,22 +202,25 @@ __global__ void __launch_bounds__(CSR_BLOCK)
           myi = indices[c0 + gl];
           myv = (float)data[c0 + gl];
         }
-        // the chunk's C^T row loads first, then the fmas, over the first E
-        // entries (E = 8, or 2 when no group of the wave has more left):
-        // lanes past a group's entries hold (0, 0.0), so a shorter group's
-        // extra entries load row 0 and add +-0 (a non-finite centre value
-        // leaves every sample undecided anyway, through B).  No exec masks;
-        // pass blocks past the slice are wave-uniform skips.
-        auto chunk = [&](auto e_tag) {
+        // the chunk's C^T row loads first, then the fmas, E entries at a
+        // time from entry h (E = EM, or 2 when no group of the wave has more
+        // left; EM x NP <= 16 loads in flight): lanes past a group's entries
+        // hold (0, 0.0), so a shorter group's extra entries load row 0 and
+        // add +-0 (a non-finite centre value leaves every sample undecided
+        // anyway, through B).  No exec masks; pass blocks past the slice are
+        // wave-uniform skips.
+        constexpr int EM = NP >= 4 ? 2 : CSR_G;
+        auto chunk = [&](auto e_tag, int h) {
           constexpr int E = decltype(e_tag)::value;
           float4 cv[E][NP];
           float vv[E];
 #pragma unroll
           for (int e = 0; e < E; ++e) {
-            const int idx = __shfl(myi, gbase + e, WAVE);
-            vv[e] = __shfl(myv, gbase + e, WAVE);
-            // element offset < 2^31: d x ks floats per slice
-            const float *row = CTs + (uint32_t)(idx * ks + jp + 4 * gl);
+            const int idx = __shfl(myi, gbase + h + e, WAVE);
+            vv[e] = __shfl(myv, gbase + h + e, WAVE);
+            // byte offset < 2^32: d x ks floats per slice (csr_run checks)
+            const float *row = (const float *)(
+                (const char *)CTs + 4u * (uint32_t)(idx * ks + jp + 4 * gl));
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
               const bool blk = p == 0 || jp + CSR_PASS * p < j_hi;
@@ -235,10 +241,14 @@ __global__ void __launch_bounds__(CSR_BLOCK)
             }
           }
         };
-        if (__any(cnt > 2))
-          chunk(std::integral_constant<int, 8>{});
-        else
-          chunk(std::integral_constant<int, 2>{});
+#pragma unroll
+        for (int h = 0; h < CSR_G; h += EM) {
+          if (h && !__any(cnt > h)) break;
+          if (__any(cnt - h > 2))
+            chunk(std::integral_constant<int, EM>{}, h);
+          else
+            chunk(std::integral_constant<int, 2>{}, h);
+        }
       }
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
@@ -518,6 +528,8 @@ static int csr_run(const int64_t *indptr, const int32_t *indices,
     op = OP_FULL_ATOMIC;  // no label array to sort (or k beyond the sort)
   const int S = csr_slices(k, d);
   const int ks = (int)csr_slice_width(k, d);
+  if ((uint64_t)d * (uint64_t)ks * 4 > 0xffffffffull)  // 32-bit gather offsets
+    return fail(DKM_E_ARG, std::string(who) + ": d x slice width beyond 4 GiB");
   // per chunk sample: S slice states (12 B), x.x and B bounds (8 B), list
   // slot (4 B)
   const int64_t chunk =
@@ -546,7 +558,9 @@ static int csr_run(const int64_t *indptr, const int32_t *indices,
                                             v.ct32, d, v.cn32,              \
                                             (int)k, S, ks, v.hdr, pst,      \
                                             pidx, pxx, pb)
-    if (npass >= 2)
+    if (npass >= 4)
+      DKM_SCREEN(4);
+    else if (npass >= 2)
       DKM_SCREEN(2);
     else
       DKM_SCREEN(1);
