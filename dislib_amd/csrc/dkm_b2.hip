@@ -900,13 +900,15 @@ __global__ void __launch_bounds__(SB2)
     // a label equal to the incoming one (the hint) needs no store; an
     // N-listed sample keeps it until k_candn writes the winner.  A sample
     // that overflowed a list keeps -1 (-(prev + 2), no previous label in
-    // this labels-only pass): the label scan finds it.  SORTED: the image's
-    // label copy follows, -1 where a re-check kernel writes the label
-    // (k_plab_sync fetches it afterwards).
+    // this labels-only pass): the label scan finds it.  SORTED: every row
+    // whose label changes or goes to a re-check gets the marker
+    // -(previous + 2) in the image's label copy; k_plab_sync fetches the
+    // final label afterwards and, on the incremental path, lists the rows
+    // that moved with their previous label.
     if (valid) {
       const bool same = unique && i1 == prv && (hint || SORTED);
       if (!nlisted && !same) lab_out[sid] = unique ? i1 : -1;
-      if (SORTED && !same) img.plab[s0 + r] = unique ? i1 : -1;
+      if (SORTED && !same) img.plab[s0 + r] = -(prv + 2);
     }
   };
 
@@ -1328,16 +1330,60 @@ __global__ void k_perm_unlabelled(const int32_t *__restrict__ lab, int64_t n,
 }
 
 // plab[i] = lab[perm[i]] (init), or only where plab[i] < 0 (sync: the rows
-// whose label a re-check kernel wrote after the screen)
-__global__ void k_plab(const int32_t *__restrict__ perm,
-                       const int32_t *__restrict__ lab, int64_t ntot,
-                       int32_t *__restrict__ plab, int only_marked) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ntot;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    if (only_marked && plab[i] >= 0) continue;
-    const int32_t p = perm[i];
-    plab[i] = p >= 0 ? lab[p] : -1;
+// the screen marked -(previous + 2)).  moved != NULL (incremental sums):
+// a synced row whose label differs from its previous one is listed in
+// moved[] (order free; *nmoved counts) and prevs[sample] = previous label.
+__global__ void __launch_bounds__(256)
+    k_plab(const int32_t *__restrict__ perm, const int32_t *__restrict__ lab,
+           int64_t ntot, int32_t *__restrict__ plab, int only_marked,
+           int32_t *__restrict__ moved, int32_t *nmoved,
+           int32_t *__restrict__ prevs) {
+  // moved rows are staged per wave in LDS and reserved with one global
+  // atomic per PLAB_BUF entries (the rows are spread over every wave: an
+  // atomic per wave and step serialised on *nmoved)
+  constexpr int PLAB_BUF = 512;
+  __shared__ int32_t buf[4][PLAB_BUF];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int32_t *wb = buf[w];
+  int cnt = 0;  // wave-uniform
+  auto flush = [&]() {
+    int at = 0;
+    if (lane == 0) at = atomicAdd(nmoved, cnt);
+    at = __shfl(at, 0, 64);
+    for (int e = lane; e < cnt; e += 64) moved[at + e] = wb[e];
+    wave_sync();
+    cnt = 0;
+  };
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // whole waves walk the range together (the ballot below)
+  for (int64_t i0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63ll;
+       i0 < ntot; i0 += stride) {
+    const int64_t i = i0 + lane;
+    bool mv = false;
+    int32_t p = -1, old = 0;
+    if (i < ntot) {
+      const int32_t cur = plab[i];
+      if (!only_marked || cur < 0) {
+        p = perm[i];
+        const int32_t nw = p >= 0 ? lab[p] : -1;
+        plab[i] = nw;
+        old = -(cur + 2);
+        mv = moved && only_marked && p >= 0 && nw != old;
+      }
+    }
+    if (!moved) continue;  // kernel-uniform
+    const uint64_t b = __ballot(mv);
+    if (!b) continue;
+    const int c = __popcll(b);
+    if (cnt + c > PLAB_BUF) flush();
+    if (mv) {
+      wb[cnt + lane_prefix(b)] = p;
+      prevs[p] = old;
+    }
+    wave_sync();
+    cnt += c;
   }
+  if (moved && cnt) flush();
 }
 
 static unsigned flat_grid(int64_t n, int cus) {
@@ -1359,7 +1405,8 @@ int launch_x_image_sorted(const TX *X, int64_t n, int d, int64_t ldx,
   const unsigned g = flat_grid(ntot, cus);
   k_perm_sorted<<<g, 256, 0, s>>>(v.sitems, v.soff + k, n, ntot, perm);
   k_perm_unlabelled<<<g, 256, 0, s>>>(labels, n, k, v.soff + k, cnt, perm);
-  k_plab<<<g, 256, 0, s>>>(perm, labels, ntot, im.plab, 0);
+  k_plab<<<g, 256, 0, s>>>(perm, labels, ntot, im.plab, 0, nullptr, nullptr,
+                           nullptr);
   if (int r = check_launch("sorted image: permutation")) return r;
   if (!acc) return launch_image_tiles<TX>(X, n, d, ldx, perm, im, cus, s);
   const int64_t nt = (n + 31) / 32;
@@ -1392,11 +1439,14 @@ template int launch_x_image_sorted<float>(const float *, int64_t, int,
                                           hipStream_t, double *);
 
 int launch_plab_sync(const XImage &img, int64_t n, const int32_t *lab,
-                     int cus, hipStream_t s) {
+                     int cus, hipStream_t s, int32_t *moved, int32_t *nmoved,
+                     int32_t *prevs) {
   if (img.kind != IMG_SORTED) return 0;
   const int64_t ntot = (n + 31) / 32 * 32;
+  if (moved && hipMemsetAsync(nmoved, 0, 4, s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "sorted image: memset");
   k_plab<<<flat_grid(ntot, cus), 256, 0, s>>>(img.perm, lab, ntot, img.plab,
-                                              1);
+                                              1, moved, nmoved, prevs);
   return check_launch("sorted image: label sync");
 }
 

@@ -2807,8 +2807,14 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const bool post = acc_kind != 0 && (!lds_fits || force_post || b1) &&
                     !AB_NO_POST &&
                     (acc_kind == 1 || (labels && nq >= n));
+  // the sorted image's incremental sums: the label sync lists the moved
+  // rows with their previous labels (in the queue scratch), so neither a
+  // copy of the labels nor a scan for changes is needed
+  const bool premoved = post && acc_kind == 2 && b1 &&
+                        img.kind == IMG_SORTED && chunk >= n &&
+                        !AB_LABEL_SUMS && sorted_sums_ok(k, n, v);
   const int32_t *prevbuf = nullptr;
-  if (post && acc_kind == 2) {
+  if (post && acc_kind == 2 && !premoved) {
     if (hipMemcpyAsync(v.queue, labels, (size_t)n * 4,
                        hipMemcpyDeviceToDevice, s) != hipSuccess)
       return fail(DKM_E_LAUNCH, "screen: label copy");
@@ -2864,11 +2870,20 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
     if ((r = launch_recheck<TX>(X, end, d, ldx, k, v, lab_out, acc,
                                 skind, vec, base, s)))
       return r;
-    // the sorted image's label copy: the rows the re-checks decided
-    if (b1 && (r = launch_plab_sync(img, n, labels, dev_info().cus, s)))
+    // the sorted image's label copy: the rows the re-checks decided (and,
+    // premoved, the list of rows that moved)
+    if (b1 && (r = launch_plab_sync(img, n, labels, dev_info().cus, s,
+                                    premoved ? v.smoved : nullptr,
+                                    premoved ? &v.hdr->nmoved : nullptr,
+                                    premoved ? v.queue : nullptr)))
       return r;
-    if (post && (r = launch_post_sums<TX>(X, base, end, d, ldx, lab_out,
-                                          prevbuf, k, acc, v, s)))
+    if (premoved) {
+      if ((r = sorted_sums_moved<TX>(X, n, d, ldx, lab_out, v.queue, k, acc,
+                                     v, s)))
+        return r;
+    } else if (post && (r = launch_post_sums<TX>(X, base, end, d, ldx,
+                                                 lab_out, prevbuf, k, acc, v,
+                                                 s)))
       return r;
   }
   return 0;

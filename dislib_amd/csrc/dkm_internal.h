@@ -201,10 +201,14 @@ inline bool x_image_sums_fused(int64_t d) {
   const int64_t nks = (d + 15) / 16;
   return nks == 1 || nks == 2 || nks == 4 || nks == 8;
 }
-// IMG_SORTED: plab <- labels[perm] where the screen marked it (-1) for a
-// re-check kernel; no-op for the other kinds
+// IMG_SORTED: plab <- labels[perm] where the screen marked it
+// (-(previous + 2)); with `moved`: the rows whose label changed are listed in
+// moved[] (count in *nmoved, zeroed here) and prevs[sample] = their previous
+// label (the incremental sums' input, sorted_sums_moved).  No-op for the
+// other kinds.
 int launch_plab_sync(const XImage &img, int64_t n, const int32_t *lab,
-                     int cus, hipStream_t s);
+                     int cus, hipStream_t s, int32_t *moved = nullptr,
+                     int32_t *nmoved = nullptr, int32_t *prevs = nullptr);
 template <class TX>
 int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
                      const WsView &v, int32_t *lab_out, int64_t base,
@@ -219,6 +223,12 @@ template <class TX>
 int sorted_sums(const TX *X, int64_t lo, int64_t hi, int d, int64_t ldx,
                 const int32_t *lab, const int32_t *prev, int k, double *acc,
                 const WsView &v, hipStream_t s);
+// Incremental sums from a moved list already built (launch_plab_sync with
+// moved = v.smoved, nmoved = &v.hdr->nmoved): +x by lab, -x by prevs.
+template <class TX>
+int sorted_sums_moved(const TX *X, int64_t n, int d, int64_t ldx,
+                      const int32_t *lab, const int32_t *prevs, int k,
+                      double *acc, const WsView &v, hipStream_t s);
 
 // Sample indices [lo, hi) grouped by lab[i] (counting sort) into v.sitems,
 // cluster c at [v.soff[c], v.soff[c + 1]) (the CSR sums, dkm_sparse.hip).

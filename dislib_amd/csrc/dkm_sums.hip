@@ -380,6 +380,29 @@ int sorted_sums(const TX *X, int64_t lo, int64_t hi, int d, int64_t ldx,
                           v, s);
 }
 
+template <class TX>
+int sorted_sums_moved(const TX *X, int64_t n, int d, int64_t ldx,
+                      const int32_t *lab, const int32_t *prevs, int k,
+                      double *acc, const WsView &v, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (!sorted_sums_ok(k, n, v))
+    return fail(DKM_E_WORKSPACE, "sorted sums: scratch too small");
+  if (int r = set_sort_lds()) return r;
+  int32_t *nmv = &v.hdr->nmoved;
+  if (int r = sort_and_sum<TX>(X, ldx, d, lab, v.smoved, nmv, n, 0, k, 1.0,
+                               acc, v, s))
+    return r;
+  return sort_and_sum<TX>(X, ldx, d, prevs, v.smoved, nmv, n, 0, k, -1.0, acc,
+                          v, s);
+}
+
+template int sorted_sums_moved<float>(const float *, int64_t, int, int64_t,
+                                      const int32_t *, const int32_t *, int,
+                                      double *, const WsView &, hipStream_t);
+template int sorted_sums_moved<double>(const double *, int64_t, int, int64_t,
+                                       const int32_t *, const int32_t *, int,
+                                       double *, const WsView &, hipStream_t);
+
 template int sorted_sums<float>(const float *, int64_t, int64_t, int, int64_t,
                                 const int32_t *, const int32_t *, int,
                                 double *, const WsView &, hipStream_t);
