@@ -30,6 +30,9 @@ for s in "$@"; do
     t_all) step t_all 900 $PT -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
+    benchprof) P=$OUT/${TAG}_benchprof; mkdir -p $P
+      step benchprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $P -o run -- python bench.py --steps 20 --warmup 3 --no-cpu
+      find $P -type f ! -name '*kernel_stats.csv' -delete 2>/dev/null; find $P -name '*kernel_stats.csv' | head -2 ;;
     c3) step c3 300 python bench.py --n 125000000 --d 64 --k 1000 --steps 8 --warmup 2 --no-cpu --only-headline ;;
     c3prof) P=$OUT/${TAG}_c3it; mkdir -p $P
       step c3prof 300 rocprofv3 --kernel-trace --stats -d $P -o run -- python bench.py --n 125000000 --d 64 --k 1000 --steps 8 --warmup 2 --no-cpu --only-headline
