@@ -190,3 +190,54 @@ def test_sorted_image_sums_fused(n, d, k, f32):
     np.add.at(scale, lab, np.abs(x.astype(np.float64)))
     assert np.all(np.abs(a[:k * d] - w[:k * d]) <=
                   1e-13 * (scale.ravel() + 1.0))
+
+
+@pytest.mark.parametrize("seed,frac_out", [(0, 0.0), (1, 0.01), (2, 0.2)])
+def test_sorted_delta_lists_the_moved_rows(seed, frac_out):
+    """The incremental pass over the label-sorted image: the label sync lists
+    the moved rows with their previous labels (no label copy, no scan), and
+    the delta is sums(new) - sums(previous) with previous labels outside
+    [0, k) contributing nothing; labels bit-exact against the oracle, and the
+    image's label copy follows them."""
+    from dislib_amd import _device, _lib
+    from dislib_amd.data import load_data
+    so = _lib.lib()
+    n, d, k = 60_000, 64, 1000
+    if not so.dkm_x_image_sorted_ok(k, d):
+        pytest.skip("(k, d) does not take the sorted image")
+    rng = np.random.default_rng(seed)
+    blobs = rng.uniform(-10, 10, (300, d))
+    x = blobs[rng.integers(0, 300, n)] + rng.standard_normal((n, d))
+    C = x[rng.choice(n, k, replace=False)] + 0.05 * rng.standard_normal((k, d))
+    prev = orc.predict_labels(x, C + 0.3 * rng.standard_normal(C.shape))
+    out = rng.random(n) < frac_out
+    prev[out] = np.where(rng.random(int(out.sum())) < 0.5, -1, k)
+    dev = torch.device("cuda", 0)
+    dd = load_data(x, subset_size=n)._device_data()
+    ws = _device.Workspace(k, d, n, dev)
+    lab = torch.from_numpy(prev.astype(np.int32)).to(dev)
+    img = _device.sorted_image(dd, lab, k, ws)
+    assert img[1] == _lib.IMAGE_SORTED
+    acc = torch.zeros(k * (d + 1), dtype=torch.float64, device=dev)
+    Ct = torch.from_numpy(C).to(dev)
+    _device.prepare(Ct, ws, acc)
+    _device.assign_delta(dd, Ct, ws, lab, acc, _lib.MODE_AUTO, image=img)
+    rl, rs, rc = orc.partial_sum(x, C)
+    got = lab.cpu().numpy()
+    assert np.array_equal(got, rl), (got != rl).sum()
+    raw = img[0].cpu().numpy()
+    nt, nks = (n + 31) // 32, (d + 15) // 16
+    tb = nt * nks * 1024
+    perm = raw[tb + nt * 128:tb + nt * 256].view(np.int32)[:n]
+    plab = raw[tb + nt * 256:tb + nt * 384].view(np.int32)[:n]
+    assert np.array_equal(plab, rl[perm])
+    a = acc.cpu().numpy()
+    ps = np.zeros((k, d))
+    pc = np.zeros(k)
+    ok = (prev >= 0) & (prev < k)
+    np.add.at(ps, prev[ok], x[ok])
+    np.add.at(pc, prev[ok], 1)
+    assert np.array_equal(a[k * d:], rc - pc)
+    err = np.max(np.abs(a[:k * d].reshape(k, d) - (rs - ps)) /
+                 np.maximum(np.abs(rs), 1.0))
+    assert err <= 1e-11
