@@ -150,12 +150,13 @@ def test_sorted_and_unsorted_fits_agree(monkeypatch, seed, blobs, std):
         assert blocks < 16 * tiles, (blocks, tiles)
 
 
-@pytest.mark.parametrize("n,d,k,f32", [(5000, 64, 300, False),
-                                       (4100, 128, 200, True),
-                                       (777, 16, 2000, False),
-                                       (3000, 40, 100, False),
-                                       (9000, 20, 64, True)])
-def test_sorted_image_sums_fused(n, d, k, f32):
+@pytest.mark.parametrize("n,d,k,f32,out", [(5000, 64, 300, False, 0.0),
+                                           (4100, 128, 200, True, 0.0),
+                                           (777, 16, 2000, False, 0.0),
+                                           (3000, 40, 100, False, 0.0),
+                                           (9000, 20, 64, True, 0.0),
+                                           (6000, 64, 500, False, 0.1)])
+def test_sorted_image_sums_fused(n, d, k, f32, out):
     """dkm_x_image_sorted_sums_*: the image of dkm_x_image_sorted_*, and acc += the dkm_label_sums_* result (fp64
     atomics: equal up to the order of the additions); d = 40 (three 16-wide
     slices) takes the image, then the separate sums."""
@@ -170,6 +171,9 @@ def test_sorted_image_sums_fused(n, d, k, f32):
         x = x.astype(np.float32)
     lab = rng.integers(0, k, n).astype(np.int32)
     lab[: n // 3] = rng.integers(0, 3, n // 3)          # a few big clusters
+    if out:       # labels outside [0, k): sorted after the others, no sums
+        m = rng.random(n) < out
+        lab[m] = np.where(rng.random(int(m.sum())) < 0.5, -1, k)
     dev = torch.device("cuda", 0)
     dd = load_data(x, subset_size=n)._device_data()
     ws = _device.Workspace(k, d, n, dev)
@@ -187,7 +191,8 @@ def test_sorted_image_sums_fused(n, d, k, f32):
     a, w = acc.cpu().numpy(), want.cpu().numpy()      # [sums k x d | counts]
     assert np.array_equal(a[k * d:], w[k * d:])
     scale = np.zeros((k, d))
-    np.add.at(scale, lab, np.abs(x.astype(np.float64)))
+    ok = (lab >= 0) & (lab < k)
+    np.add.at(scale, lab[ok], np.abs(x[ok].astype(np.float64)))
     assert np.all(np.abs(a[:k * d] - w[:k * d]) <=
                   1e-13 * (scale.ravel() + 1.0))
 
