@@ -307,6 +307,12 @@ def sorted_image_ok(dd, k):
     takes a label-sorted image (dkm_x_image_sorted_ok)?"""
     if dd.sparse or dd.n == 0 or not X_IMAGE:
         return False
+    # the screen that maintains the image reads 16-B pieces of X's rows
+    # (dkm_dense.hip launch_screen `vec`): rows a multiple of 16 B apart,
+    # X 16-B aligned (d % 8 == 0 is checked by dkm_x_image_sorted_ok)
+    isz = dd.X.element_size()
+    if (dd.X.stride(0) * isz) % 16 or dd.X.data_ptr() % 16:
+        return False
     so = _lib.lib()
     return (int(so.dkm_x_image_kind(int(k), dd.d, _lib.MODE_AUTO)) ==
             _lib.IMAGE_SINGLE and bool(so.dkm_x_image_sorted_ok(int(k), dd.d)))
@@ -418,9 +424,20 @@ def rechecked(ws):
 
 def screen_counters(ws):
     """(threshold-pass tiles, tiles it decided, centre blocks screened over
-    the label-sorted image) accumulated over the workspace's life."""
+    the label-sorted image, sorted-image tiles the steady-state pass handed
+    to the general one) accumulated over the workspace's life."""
     so = _lib.lib()
-    out = (ctypes.c_int64 * 3)()
+    out = (ctypes.c_int64 * 4)()
     _lib.check(so.dkm_screen_counters(ws.p, out, stream_ptr()),
                "dkm_screen_counters")
+    return tuple(int(x) for x in out)
+
+
+def screen_lists(ws):
+    """(re-check list, two-candidate, 3..6-candidate entries, overflowed
+    samples) the last single-product screen launch left (diagnostics)."""
+    so = _lib.lib()
+    out = (ctypes.c_int64 * 4)()
+    _lib.check(so.dkm_screen_lists(ws.p, ws.nbytes, out, stream_ptr()),
+               "dkm_screen_lists")
     return tuple(int(x) for x in out)

@@ -84,6 +84,8 @@ SIGNATURES = {
                                   _f64, _p, _p]),
     "dkm_screen_stats": (_i32, [_p, ctypes.POINTER(_i64), _p]),
     "dkm_screen_counters": (_i32, [_p, ctypes.POINTER(_i64), _p]),
+    "dkm_screen_lists": (_i32, [_p, ctypes.c_size_t, ctypes.POINTER(_i64),
+                                _p]),
     # distance-primitive reuse (kNN, DBSCAN epsilon query)
     "dkm_knn_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "dkm_knn_f64": (_i32, [_p, _i64, _i64, _p, _i64, _i64, _i64, _i64, _p,

@@ -52,8 +52,7 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "dkm_internal.h"
-#include "dkm_screen.h"
+#include "dkm_b2.h"
 
 namespace dkm {
 
@@ -66,9 +65,11 @@ namespace dkm {
 #define DKM_AB_B2_PROBE 0
 #endif
 constexpr int SB2 = DKM_AB_SB2;
-constexpr uint32_t PACK2 = 9, PACK2_MASK = (1u << PACK2) - 1;
-constexpr int B2_ENT = 3;    // kept (score, centre) per sample besides p
-constexpr int B2_RTHR = 4;   // over-full samples a wave tolerates per tile
+// A/B: the sorted image's steady state on this kernel alone (no
+// k_screen_sorted)
+#ifndef DKM_AB_NO_SORTED_FAST
+#define DKM_AB_NO_SORTED_FAST 0
+#endif
 // per-wave LDS scratch: -T[32], hint[32], count[32], |x|^2[32], the tile
 // transpose (32 rows x 16 bf16 features, 1 KB; the kept entries
 // [32][B2_ENT] reuse it after the tile's conversion), then 32 x nkw
@@ -76,61 +77,6 @@ constexpr int B2_RTHR = 4;   // over-full samples a wave tolerates per tile
 constexpr int B2_SCR_FIXED = 4 * 128 + 1024;
 static_assert(32 * B2_ENT * 8 + 128 <= 1024,
               "kept entries and s_hat_p fit the transpose");
-
-// v_min3 / v_min without fminf's NaN canonicalisation (inline asm: the
-// compiler would insert v_max_f32 x, x on every MFMA result)
-__device__ __forceinline__ float vmin3(float a, float b, float c) {
-  float r;
-  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-__device__ __forceinline__ float vmin2(float a, float b) {
-  float r;
-  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-
-// min of an accumulator's 16 values: one asm statement, so that the
-// compiler pads no hazard nops between the dependent steps (separate asm
-// statements got an s_nop each; plain VALU RAW needs none)
-template <class V16>
-__device__ __forceinline__ float min16(const V16 &a) {
-  float r, t0, t1, t2, t3, t4;
-  asm("v_min3_f32 %1, %6, %7, %8\n\t"
-      "v_min3_f32 %2, %9, %10, %11\n\t"
-      "v_min3_f32 %3, %12, %13, %14\n\t"
-      "v_min3_f32 %4, %15, %16, %17\n\t"
-      "v_min3_f32 %5, %18, %19, %20\n\t"
-      "v_min3_f32 %1, %1, %2, %3\n\t"
-      "v_min3_f32 %4, %4, %5, %21\n\t"
-      "v_min_f32 %0, %1, %4"
-      : "=v"(r), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4)
-      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]),
-        "v"(a[6]), "v"(a[7]), "v"(a[8]), "v"(a[9]), "v"(a[10]), "v"(a[11]),
-        "v"(a[12]), "v"(a[13]), "v"(a[14]), "v"(a[15]));
-  return r;
-}
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// the workspace pointers the kernel reads (the whole WsView as a kernel
-// argument kept ~60 SGPRs of unused pointers live: 82 SGPRs spilled)
-struct B2View {
-  WsHeader *hdr;
-  const uint16_t *b1frag;
-  const float *cn32f, *cn32;
-  int2 *tlist, *clist;
-  int4 *nlist;
-  int32_t *tcount, *ccount, *ncount;
-  // block skipping (IMG_SORTED): mind[p * MIND_LD + cb] = a lower bound on
-  // min_{j in block cb, j != p} |c_p - c_j| (dkm_util.hip k_mind); nullptr
-  // = no skipping
-  const float *mind;
-};
 
 // IMG: IMG_NONE (X converted in the kernel), IMG_SINGLE (the resident bf16
 // image, sample order) or IMG_SORTED (the same image with its rows grouped
@@ -140,9 +86,13 @@ template <class TX, int NKS, bool W1, int IMG>
 __global__ void __launch_bounds__(SB2)
     k_screen_b2(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
                 B2View v, int32_t *__restrict__ lab_out, int64_t base,
-                int hint, XImage img) {
+                int hint, XImage img, const int32_t *__restrict__ tlst,
+                const uint32_t *tlst_n) {
   typedef float f32x16 __attribute__((ext_vector_type(16)));
   constexpr bool SORTED = IMG == IMG_SORTED;
+  // tile-list mode (the tiles k_screen_sorted handed over): nothing to do
+  // unless it listed some
+  if (tlst && *tlst_n == 0) return;
   constexpr int GB = 1 << (PACK2 - 4);  // 32-centre blocks per top-3 group
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int nkb = (int)(kpad32(k) / 32);
@@ -558,7 +508,7 @@ __global__ void __launch_bounds__(SB2)
           // 7 v_min3 + 1 v_min on the raw MFMA results (no NaN
           // canonicalisation: a NaN score comes with a NaN threshold, and
           // its sample is rejected by the `sane` test)
-          any = min16(acc) <= thr;
+          any = min16(acc, ninf) <= thr;
           if (DKM_AB_B2_PROBE == 2) any = acc[0] == 12345.f;  // (invalid)
         };
         auto append = [&](int cb, const f32x16 &acc, float thr, float nc,
@@ -908,11 +858,35 @@ __global__ void __launch_bounds__(SB2)
     if (valid) {
       const bool same = unique && i1 == prv && (hint || SORTED);
       if (!nlisted && !same) lab_out[sid] = unique ? i1 : -1;
-      if (SORTED && !same) img.plab[s0 + r] = -(prv + 2);
+      // (a previous label outside [0, k) is marked as -1: -(prv + 2) of
+      // such a label could fall on a label or past INT32_MIN)
+      if (SORTED && !same)
+        img.plab[s0 + r] = -(((unsigned)prv < (unsigned)k ? prv : -1) + 2);
     }
   };
 
   if constexpr (IMG != IMG_NONE) {
+   if (tlst) {
+    // ---- tile-list mode: the listed image tiles, appended to the lists
+    // k_screen_sorted left (same segments)
+    if (listing) {
+      tl_cnt = v.tcount[wv];
+      cl_cnt = v.ccount[wv];
+      nl_cnt = v.ncount[wv];
+    }
+    const int64_t nls = *tlst_n;
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      atomicAdd((unsigned long long *)&v.hdr->sfall_total,
+                (unsigned long long)nls);
+    for (int64_t i = wv; i < nls; i += (int64_t)gridDim.x * NW) {
+      const int64_t s0 = (int64_t)tlst[i] * 32;
+      load_img(s0, xq, xxq, pq, sq);
+      bf16x8 xh[NKS];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) xh[ks] = xq[ks];
+      process(s0, xh, xxq, pq, sq);
+    }
+   } else {
     // ---- sample image: the next tile's loads are in flight while this one
     // is screened (LATEPF: issued from process() after the block loop)
     int64_t s0 = base + wv * 32;
@@ -932,6 +906,7 @@ __global__ void __launch_bounds__(SB2)
       process(s0, xh, xx, prv, sid);
       late_prefetch();
     }
+   }
   } else {
   for (int64_t s0 = base + wv * 32; s0 < n; s0 += step) {
     load_tile(s0);
@@ -981,6 +956,9 @@ __global__ void __launch_bounds__(SB2)
     process(s0, xh, xx, pv, s0 + r < n ? (int)(s0 + r) : -1);
   }
   }  // IMG_NONE
+  if (!tlst && wv == 0 && lane == 0)
+    v.hdr->lseg = (int32_t)std::min<int64_t>((int64_t)gridDim.x * NW,
+                                             std::min(TL_SEGS, B1_SEGS));
   if (lane == 0 && listing) {
     v.tcount[wv] = tl_cnt;
     v.ccount[wv] = cl_cnt;
@@ -1335,7 +1313,7 @@ __global__ void k_perm_unlabelled(const int32_t *__restrict__ lab, int64_t n,
 // moved[] (order free; *nmoved counts) and prevs[sample] = previous label.
 __global__ void __launch_bounds__(256)
     k_plab(const int32_t *__restrict__ perm, const int32_t *__restrict__ lab,
-           int64_t ntot, int32_t *__restrict__ plab, int only_marked,
+           int64_t ntot, int k, int32_t *__restrict__ plab, int only_marked,
            int32_t *__restrict__ moved, int32_t *nmoved,
            int32_t *__restrict__ prevs) {
   // moved rows are staged per wave in LDS and reserved with one global
@@ -1366,7 +1344,9 @@ __global__ void __launch_bounds__(256)
       if (!only_marked || cur < 0) {
         p = perm[i];
         const int32_t nw = p >= 0 ? lab[p] : -1;
-        plab[i] = nw;
+        // a label outside [0, k) is kept as -1: a negative copy is read as
+        // the marker -(previous + 2), and -1 means "no previous label"
+        plab[i] = (unsigned)nw < (unsigned)k ? nw : -1;
         old = -(cur + 2);
         mv = moved && only_marked && p >= 0 && nw != old;
       }
@@ -1405,8 +1385,8 @@ int launch_x_image_sorted(const TX *X, int64_t n, int d, int64_t ldx,
   const unsigned g = flat_grid(ntot, cus);
   k_perm_sorted<<<g, 256, 0, s>>>(v.sitems, v.soff + k, n, ntot, perm);
   k_perm_unlabelled<<<g, 256, 0, s>>>(labels, n, k, v.soff + k, cnt, perm);
-  k_plab<<<g, 256, 0, s>>>(perm, labels, ntot, im.plab, 0, nullptr, nullptr,
-                           nullptr);
+  k_plab<<<g, 256, 0, s>>>(perm, labels, ntot, k, im.plab, 0, nullptr,
+                           nullptr, nullptr);
   if (int r = check_launch("sorted image: permutation")) return r;
   if (!acc) return launch_image_tiles<TX>(X, n, d, ldx, perm, im, cus, s);
   const int64_t nt = (n + 31) / 32;
@@ -1438,15 +1418,16 @@ template int launch_x_image_sorted<float>(const float *, int64_t, int,
                                           const WsView &, void *, int,
                                           hipStream_t, double *);
 
-int launch_plab_sync(const XImage &img, int64_t n, const int32_t *lab,
+int launch_plab_sync(const XImage &img, int64_t n, int k, const int32_t *lab,
                      int cus, hipStream_t s, int32_t *moved, int32_t *nmoved,
                      int32_t *prevs) {
   if (img.kind != IMG_SORTED) return 0;
   const int64_t ntot = (n + 31) / 32 * 32;
   if (moved && hipMemsetAsync(nmoved, 0, 4, s) != hipSuccess)
     return fail(DKM_E_LAUNCH, "sorted image: memset");
-  k_plab<<<flat_grid(ntot, cus), 256, 0, s>>>(img.perm, lab, ntot, img.plab,
-                                              1, moved, nmoved, prevs);
+  k_plab<<<flat_grid(ntot, cus), 256, 0, s>>>(img.perm, lab, ntot, k,
+                                              img.plab, 1, moved, nmoved,
+                                              prevs);
   return check_launch("sorted image: label sync");
 }
 
@@ -1463,6 +1444,20 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
     return fail(DKM_E_ARG, "screen_b2: the sorted image needs the whole range");
   if (ik == IMG_SINGLE && base % 32 != 0) ik = IMG_NONE;
   if (ik != IMG_SINGLE && ik != IMG_SORTED) ik = IMG_NONE;
+  // the steady state over the sorted image: k_screen_sorted, then this
+  // kernel over the tiles it listed (the fit's moved-list scratch holds the
+  // list: it is filled only after the screen, by the label sync)
+  const int32_t *tlst = nullptr;
+  const uint32_t *tlst_n = nullptr;
+  if (ik == IMG_SORTED && hint == 1 && !DKM_AB_NO_SORTED_FAST) {
+    const int r = launch_screen_sorted(end, d, k, v, lab_out, img, cus, s,
+                                       nseg, v.smoved, &v.hdr->sfall);
+    if (r > 1 || r < 0) return r;
+    if (r == 0) {
+      tlst = v.smoved;
+      tlst_n = &v.hdr->sfall;
+    }
+  }
   const int nks = (int)(dpad16(d) / 16);
   const bool w1 = kpad32(k) <= 1024;
   const void *kf = nullptr;
@@ -1487,26 +1482,23 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
                           (int)lds) != hipSuccess)
     return fail(DKM_E_LAUNCH, "screen_b2: LDS attribute");
   const int nw = SB2 / 64;  // screening waves
-  const int64_t need = (end - base + 32 * nw - 1) / (32 * nw);
-  const unsigned g =
-      (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)cus));
-  *nseg = (int)std::min<int64_t>((int64_t)g * nw, std::min(TL_SEGS, B1_SEGS));
-  B2View bv;
-  bv.hdr = v.hdr;
-  bv.b1frag = v.b1frag;
-  bv.cn32f = v.cn32f;
-  bv.cn32 = v.cn32;
-  bv.tlist = v.tlist;
-  bv.clist = v.clist;
-  bv.nlist = v.nlist;
-  bv.tcount = v.tcount;
-  bv.ccount = v.ccount;
-  bv.ncount = v.ncount;
-  bv.mind = ik == IMG_SORTED ? v.mind : nullptr;
+  unsigned g;
+  if (tlst) {
+    // tile-list mode: the waves append to k_screen_sorted's list segments
+    // (no more waves than it had)
+    g = (unsigned)std::max(1, *nseg / nw);
+  } else {
+    const int64_t need = (end - base + 32 * nw - 1) / (32 * nw);
+    g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, (int64_t)cus));
+    *nseg =
+        (int)std::min<int64_t>((int64_t)g * nw, std::min(TL_SEGS, B1_SEGS));
+  }
+  const B2View bv = b2_view(v, ik == IMG_SORTED);
   hipLaunchKernelGGL((void (*)(const TX *, int64_t, int, int64_t, int, B2View,
-                               int32_t *, int64_t, int, XImage))kf,
+                               int32_t *, int64_t, int, XImage,
+                               const int32_t *, const uint32_t *))kf,
                      dim3(g), dim3(SB2), lds, s, X, end, d, ldx, k, bv,
-                     lab_out, base, hint, img);
+                     lab_out, base, hint, img, tlst, tlst_n);
   return check_launch("screen assignment (single product, centres on lanes)");
 }
 

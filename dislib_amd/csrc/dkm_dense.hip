@@ -2872,7 +2872,7 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
       return r;
     // the sorted image's label copy: the rows the re-checks decided (and,
     // premoved, the list of rows that moved)
-    if (b1 && (r = launch_plab_sync(img, n, labels, dev_info().cus, s,
+    if (b1 && (r = launch_plab_sync(img, n, k, labels, dev_info().cus, s,
                                     premoved ? v.smoved : nullptr,
                                     premoved ? &v.hdr->nmoved : nullptr,
                                     premoved ? v.queue : nullptr)))
@@ -3173,7 +3173,10 @@ int dkm_x_image_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
 }
 
 int dkm_x_image_sorted_ok(int64_t k, int64_t d) {
-  return k > 1 && k <= INT32_MAX && d > 0 && d <= 128 &&
+  // the single-product screen that keeps the image's label copy needs
+  // 16-B sample rows (launch_screen's `vec`; the caller checks the row
+  // stride and alignment of X)
+  return k > 1 && k <= INT32_MAX && d > 0 && d <= 128 && d % 8 == 0 &&
                  dkm_x_image_kind(k, d, DKM_MODE_SCREEN_BF16) == IMG_SINGLE &&
                  mind_ok(k, d)
              ? 1

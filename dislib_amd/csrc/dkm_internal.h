@@ -39,9 +39,17 @@ struct WsHeader {
   uint32_t csr_nund;        // CSR screen: undecided samples of this chunk
   uint32_t pad2;
   uint64_t reserved[5];
+  // k_screen_sorted: tiles handed to k_screen_b2 this call / in all calls
+  uint32_t sfall;
+  uint32_t qhead;  // k_screen_sorted: next chunk of image tiles (zeroed
+                   // with sfall before each launch)
+  int32_t lseg;    // list segments of the last single-product screen launch
+  int32_t pad3;
+  uint64_t sfall_total;
 };
 constexpr uint64_t WS_MAGIC = 0x444b4d5753303033ull;  // "DKMWS003"
 constexpr size_t WS_HDR = 256;
+static_assert(sizeof(WsHeader) <= WS_HDR, "the header fits WS_HDR");
 
 __host__ __device__ inline int64_t round_up(int64_t a, int64_t b) {
   return (a + b - 1) / b * b;
@@ -73,8 +81,8 @@ __host__ __device__ inline int64_t ct_ld(int64_t k) { return (k + 15) / 16 * 16;
 // entries of (offset, c1 | c2 << 16)), three or more to the re-check lists.
 // ---------------------------------------------------------------------------
 constexpr int B1_SEGS = 4096;          // >= 256 CUs x 8 waves
-constexpr int B1_CAP = 4096;           // candidate entries per screen wave
-constexpr int B1_NCAP = 1024;          // 3..6-candidate entries per wave
+constexpr int B1_CAP = 8192;           // candidate entries per screen wave
+constexpr int B1_NCAP = 2048;          // 3..6-candidate entries per wave
 constexpr size_t B1_LDS_MAX = 150 * 1024;
 constexpr size_t B1_LDS_POISON_MAX = 160 * 1024;  // with the poisoned norms
 
@@ -206,7 +214,7 @@ inline bool x_image_sums_fused(int64_t d) {
 // moved[] (count in *nmoved, zeroed here) and prevs[sample] = their previous
 // label (the incremental sums' input, sorted_sums_moved).  No-op for the
 // other kinds.
-int launch_plab_sync(const XImage &img, int64_t n, const int32_t *lab,
+int launch_plab_sync(const XImage &img, int64_t n, int k, const int32_t *lab,
                      int cus, hipStream_t s, int32_t *moved = nullptr,
                      int32_t *nmoved = nullptr, int32_t *prevs = nullptr);
 template <class TX>
@@ -238,7 +246,7 @@ int sort_by_label(const int32_t *lab, int64_t lo, int64_t hi, int k,
 // Per-wave lists of the screen's undecided samples (resolved by
 // k_recheck_list without scanning the labels): one segment of TL_CAP
 // entries per screen wave, TL_SEGS >= 256 CUs x 32 waves.
-constexpr int TL_CAP = 1024;
+constexpr int TL_CAP = 2048;
 constexpr int TL_SEGS = 8192;
 
 // CSR screen (dkm_sparse.hip): the centres are cut into S slices (a power

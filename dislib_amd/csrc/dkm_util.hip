@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "dkm_internal.h"
 
@@ -563,6 +564,38 @@ int dkm_screen_counters(const void *ws, int64_t *out, void *stream) {
                             hipGetErrorString(e));
   if (h.magic != WS_MAGIC) return fail(DKM_E_ARG, "screen_counters: bad ws");
   for (int i = 0; i < 3; ++i) out[i] = (int64_t)h.reserved[i];
+  out[3] = (int64_t)h.sfall_total;
+  return 0;
+}
+
+int dkm_screen_lists(const void *ws, size_t ws_bytes, int64_t *out,
+                     void *stream) {
+  if (!ws || !out) return fail(DKM_E_ARG, "screen_lists: NULL");
+  hipStream_t s = (hipStream_t)stream;
+  WsHeader h;
+  hipError_t e = hipMemcpyAsync(&h, ws, sizeof(h), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess)
+    return fail((int)e, std::string("screen_lists: ") + hipGetErrorString(e));
+  if (h.magic != WS_MAGIC) return fail(DKM_E_ARG, "screen_lists: bad ws");
+  WsView v;
+  if (int r = ws_view(ws, ws_bytes, h.k, h.d, &v)) return r;
+  for (int i = 0; i < 4; ++i) out[i] = 0;
+  out[3] = (int64_t)h.qcount;
+  const int nseg = std::max(0, std::min(h.lseg, TL_SEGS));
+  if (nseg == 0) return 0;
+  std::vector<int32_t> c(nseg);
+  int32_t *src[3] = {v.tcount, v.ccount, v.ncount};
+  for (int a = 0; a < 3; ++a) {
+    if (!src[a] || (a > 0 && nseg > B1_SEGS)) continue;
+    e = hipMemcpyAsync(c.data(), src[a], (size_t)nseg * 4,
+                       hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess)
+      return fail((int)e, std::string("screen_lists: ") +
+                              hipGetErrorString(e));
+    for (int i = 0; i < nseg; ++i) out[a] += c[i];
+  }
   return 0;
 }
 

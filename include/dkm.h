@@ -330,8 +330,16 @@ int dkm_screen_stats(const void *ws, int64_t *n_rechecked, void *stream);
 /* Single-product screen counters over the workspace's life (host, syncs
  * `stream`): out[0] tiles given the threshold pass, out[1] tiles it
  * decided (the rest took the top-3 pass), out[2] 32-centre blocks screened
- * by threshold passes over the label-sorted image (DKM_IMAGE_SORTED).     */
+ * by threshold passes over the label-sorted image (DKM_IMAGE_SORTED),
+ * out[3] tiles of that image the steady-state pass handed to the general
+ * one (out has 4 entries).                                                 */
 int dkm_screen_counters(const void *ws, int64_t *out, void *stream);
+/* The lists the last single-product screen launch left (host, syncs
+ * `stream`; diagnostics): out[0] samples for the exact re-check list,
+ * out[1] two-candidate entries, out[2] 3..6-candidate entries, out[3]
+ * samples that overflowed a list (found by the label scan).               */
+int dkm_screen_lists(const void *ws, size_t ws_bytes, int64_t *out,
+                     void *stream);
 
 /* Build flags of this library: 0 for a product build.  Non-zero
  * (DKM_BUILD_TIMING_ONLY) when it was compiled with an A/B timing probe

@@ -24,7 +24,7 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("n,d,k", [(1000, 64, 300), (77, 20, 40),
+@pytest.mark.parametrize("n,d,k", [(1000, 64, 300), (77, 24, 40),
                                    (4100, 128, 200), (64, 16, 2000)])
 def test_sorted_image_layout(n, d, k):
     """Rows grouped by label (labels outside [0, k) after them, -1 past n),
@@ -62,7 +62,9 @@ def _check_sorted_layout(raw, x, lab, k):
     m = int(ok.sum())
     assert ok[:m].all() and not ok[m:].any()              # unlabelled last
     assert np.all(np.diff(lp[:m]) >= 0)                   # grouped, in order
-    assert np.array_equal(plab[:n], lp)
+    # the label copy holds labels outside [0, k) as -1 (a negative copy is
+    # read as a re-check marker by the label sync)
+    assert np.array_equal(plab[:n], np.where((lp >= 0) & (lp < k), lp, -1))
     f = np.zeros((nt * 32, nks * 16), np.float32)
     f[:n, :d] = x[p].astype(np.float32)
     u = f.view(np.uint32).astype(np.uint64)
@@ -144,7 +146,8 @@ def test_sorted_and_unsorted_fits_agree(monkeypatch, seed, blobs, std):
     err = np.max(np.abs(out[True][1] - out[False][1]) /
                  np.maximum(np.abs(out[False][1]), 1.0))
     assert err <= 1e-12
-    tiles, done, blocks = out[True][2]
+    tiles, done, blocks, handed = out[True][2]
+    assert 0 <= handed <= tiles
     assert 0 < blocks <= 32 * tiles
     if blobs == 1000:       # separated blobs: most blocks are cleared
         assert blocks < 16 * tiles, (blocks, tiles)
@@ -154,7 +157,7 @@ def test_sorted_and_unsorted_fits_agree(monkeypatch, seed, blobs, std):
                                            (4100, 128, 200, True, 0.0),
                                            (777, 16, 2000, False, 0.0),
                                            (3000, 40, 100, False, 0.0),
-                                           (9000, 20, 64, True, 0.0),
+                                           (9000, 24, 64, True, 0.0),
                                            (6000, 64, 500, False, 0.1)])
 def test_sorted_image_sums_fused(n, d, k, f32, out):
     """dkm_x_image_sorted_sums_*: the image of dkm_x_image_sorted_*, and acc += the dkm_label_sums_* result (fp64
@@ -216,7 +219,11 @@ def test_sorted_delta_lists_the_moved_rows(seed, frac_out):
     C = x[rng.choice(n, k, replace=False)] + 0.05 * rng.standard_normal((k, d))
     prev = orc.predict_labels(x, C + 0.3 * rng.standard_normal(C.shape))
     out = rng.random(n) < frac_out
-    prev[out] = np.where(rng.random(int(out.sum())) < 0.5, -1, k)
+    # previous labels outside [0, k), including markers' own range (-2,
+    # INT32_MIN): they contribute nothing and the rows are listed as moved
+    u = rng.random(int(out.sum()))
+    prev[out] = np.where(u < 0.25, -1, np.where(u < 0.5, k, np.where(
+        u < 0.75, -2, np.iinfo(np.int32).min)))
     dev = torch.device("cuda", 0)
     dd = load_data(x, subset_size=n)._device_data()
     ws = _device.Workspace(k, d, n, dev)
@@ -246,3 +253,39 @@ def test_sorted_delta_lists_the_moved_rows(seed, frac_out):
     err = np.max(np.abs(a[:k * d].reshape(k, d) - (rs - ps)) /
                  np.maximum(np.abs(rs), 1.0))
     assert err <= 1e-11
+
+
+@pytest.mark.parametrize("d,ldx", [(60, 60), (64, 65), (64, 66)])
+def test_fit_shapes_without_the_sorted_image(d, ldx):
+    """Auto-mode fits whose samples the single-product screen cannot read as
+    16-B pieces (d % 8 != 0, or rows 8 B apart): no sorted image is built,
+    and the fit matches the oracle (it used to fail with DKM_E_ARG at the
+    first iteration over the image)."""
+    from dislib_amd.cluster.kmeans import KMeans, _Lloyd, _init_centers
+    from dislib_amd.data import Dataset, Subset
+    n, k = 20_000, 1000
+    rng = np.random.default_rng(d + ldx)
+    blobs = rng.uniform(-10, 10, (200, d))
+    xw = np.zeros((n, ldx))
+    xw[:, :d] = blobs[rng.integers(0, 200, n)] + rng.standard_normal((n, d))
+    dev = torch.device("cuda", 0)
+    Xw = torch.from_numpy(xw).to(dev)
+    ds = Dataset(n_features=d)
+    ds.append(Subset(Xw[:, :d]))
+    st = _Lloyd(ds, _init_centers(d, False, k, 3), 0.0, True, "auto", dev)
+    # (a strided view is copied to 16-B rows on upload: then the image is
+    # legal; d % 8 != 0 never takes it)
+    assert not (st.sorting and d % 8)
+    for _ in range(4):
+        st.step()
+    x = xw[:, :d]
+    C = _init_centers(d, False, k, 3)
+    for _ in range(4):
+        lab, s, c = orc.partial_sum(x, C)
+        nz = c > 0
+        C = C.copy()
+        C[nz] = s[nz] / c[nz, None]
+    got = st.labels[:n].cpu().numpy()
+    assert np.array_equal(got, lab), (got != lab).sum()
+    err = np.max(np.abs(st.C.cpu().numpy() - C) / np.maximum(np.abs(C), 1.0))
+    assert err <= 1e-9

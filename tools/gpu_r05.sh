@@ -1,0 +1,46 @@
+#!/bin/bash
+# Round-5 GPU session steps (each GPU step under its own time limit; a
+# crash / timeout / fault stops the session).  usage: gpu_r05.sh TAG STEP...
+#   t_sorted  sorted-image / b2 / C3 full-size label tests
+#   t_all     the whole GPU suite
+#   diag      tools/c3_diag.py on the main library and on libdkm_old.so
+#   c3it      C3 bench line under a rocprofv3 kernel trace, per iteration
+#   c3ab      C3 bench line, main vs libdkm_old.so, two rounds
+#   bench     default bench.py
+TAG=${1:-r05}; shift
+OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+step() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 $lim "$@" > $OUT/${TAG}_${name}.log 2>&1
+  local rc=$?
+  tail -4 $OUT/${TAG}_${name}.log | cut -c1-400
+  echo "== $name rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name"; exit $rc; fi
+  return 0
+}
+PT="python -u -m pytest -p no:cacheprovider --timeout 200 --timeout-method thread -q"
+C3="python bench.py --n 125000000 --d 64 --k 1000 --steps 8 --warmup 2 --no-cpu --only-headline"
+OLD=$PWD/dislib_amd/libdkm_old.so
+for s in "$@"; do
+  case $s in
+    t_sorted) step t_sorted 900 $PT tests/test_gpu_sorted.py tests/test_gpu_b2.py tests/test_gpu_fullsize.py::test_c3_full_size_labels ;;
+    t_all) step t_all 1100 $PT -m gpu tests ;;
+    diag) step diag_main 240 python tools/c3_diag.py
+          DKM_LIB=$OLD step diag_old 240 python tools/c3_diag.py ;;
+    c3it) P=$OUT/${TAG}_c3it; mkdir -p $P
+      step c3it 300 rocprofv3 --kernel-trace --stats -d $P -o run -- $C3
+      DB=$(find $P -name '*.db' | head -1)
+      [ -n "$DB" ] && python tools/prof_iters.py $DB > $P/iters.txt 2>&1 && rm -f $DB
+      find $P -type f ! -name 'iters.txt' ! -name '*kernel_stats.csv' -delete
+      cut -c1-300 $P/iters.txt ;;
+    c3ab) for r in 1 2; do for v in main old; do
+        if [ $v = old ]; then export DKM_LIB=$OLD; else unset DKM_LIB; fi
+        step c3_$v$r 300 $C3
+        python -c "import json;d=json.loads([l for l in open('$OUT/${TAG}_c3_$v$r.log') if l.startswith('{')][-1]);print('$v', round(d['ms_per_step'],3), 'fit', round(d['fit_ms_per_iter'],2), 'kern', round(d['roofline']['kernel_ms'],3))"
+      done; done; unset DKM_LIB ;;
+    bench) step bench 900 python bench.py ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== done"
