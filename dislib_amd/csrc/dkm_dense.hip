@@ -1901,60 +1901,6 @@ __device__ __forceinline__ double leaf8_share(const double (&xv)[16],
   return r;
 }
 
-// Two-candidate samples of k_screen_b1: the reference arithmetic (numpy
-// pairwise order, correctly rounded sqrt) on c1 and c2, first index among
-// equal distances.  Labels only.  k_screen_b1 runs only for 8 <= d <= 128
-// with d % 8 == 0, where numpy's sum is one pairwise leaf: 8 accumulators
-// r_j = sum_i f(j + 8 i) combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)).
-// Lane (e, c, j) = (lane >> 4, (lane >> 3) & 1, lane & 7) keeps r_j of
-// candidate c of entry e, so the 8 lanes of a candidate read 64 contiguous
-// bytes per step (a lane-per-entry walk read one 8-B word per lane from 64
-// scattered rows); the combine tree is three xor shuffles (IEEE addition is
-// commutative, so both partners of a pair hold the same bits).
-template <class TX>
-__global__ void __launch_bounds__(BLOCK)
-    k_cand2(const TX *__restrict__ X, int d, int64_t ldx,
-            const double *__restrict__ C, WsView v,
-            int32_t *__restrict__ lab_out, int64_t base, int nseg) {
-  const int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
-  const int64_t nwv = (int64_t)gridDim.x * (BLOCK / 64);
-  const int lane = threadIdx.x & 63;
-  const int e = lane >> 4, cs = (lane >> 3) & 1, j = lane & 7;
-  const int nst = d >> 3;
-  unsigned long long mine = 0;
-  // (segment, 64-entry batch) pairs over all waves, batch index major
-  for (int64_t L = wv; L < (int64_t)nseg * (B1_CAP / 64); L += nwv) {
-    const int64_t sg = L % nseg;
-    const int t0 = (int)(L / nseg) * 64;
-    const int cnt = v.ccount[sg];
-    if (t0 == 0 && lane == 0) mine += cnt;
-    if (t0 >= cnt) continue;  // wave-uniform
-    const int2 *list = v.clist + sg * B1_CAP + t0;
-    const int m = min(64, cnt - t0);
-    const int2 own = list[min(lane, m - 1)];  // the batch, one entry a lane
-    for (int p = 0; p < m; p += 4) {
-      const bool live = p + e < m;
-      const int src = min(p + e, m - 1);
-      const int2 it = make_int2(__shfl(own.x, src, 64), __shfl(own.y, src, 64));
-      const int c1 = it.y & 0xffff, c2 = (int)((unsigned)it.y >> 16);
-      const int64_t si = base + it.x;
-      const TX *xr = X + si * ldx + j;
-      const double *cr = C + (int64_t)(cs ? c2 : c1) * d + j;
-      double xv[16];
-      leaf8_load_x(xr, nst, xv);
-      double r = leaf8_share(xv, cr, nst);
-      r = r + __shfl_xor(r, 1, 64);
-      r = r + __shfl_xor(r, 2, 64);
-      r = r + __shfl_xor(r, 4, 64);
-      const double dist = argmin_key(sqrt(r));
-      const double o = __shfl_xor(dist, 8, 64);  // the other candidate
-      if (live && cs == 0 && j == 0)
-        lab_out[si] = (o < dist || (o == dist && c2 < c1)) ? c2 : c1;
-    }
-  }
-  if (mine) atomicAdd((unsigned long long *)&v.hdr->rechecked_total, mine);
-}
-
 // 3..6-candidate samples of k_screen_b1's threshold pass: the reference
 // arithmetic on exactly those centres (every other centre is strictly
 // farther), best by (distance, index).  8 lanes per distance in numpy's
@@ -2741,13 +2687,11 @@ template <class TX>
 static int launch_cand2(const TX *X, int d, int64_t ldx, const double *C,
                         const WsView &v, int32_t *lab_out, int64_t base,
                         int nseg, hipStream_t s) {
-  const int64_t units = (int64_t)nseg * (B1_CAP / 64);
-  const int64_t g = std::max<int64_t>(
-      1, std::min<int64_t>((int64_t)dev_info().cus * 8,
-                           (units + BLOCK / 64 - 1) / (BLOCK / 64)));
-  k_cand2<TX><<<(unsigned)g, BLOCK, 0, s>>>(X, d, ldx, C, v, lab_out, base,
-                                            nseg);
-  return check_launch("two-candidate re-check");
+  // dkm_cand.hip (the screens list two-candidate samples only for
+  // d % 8 == 0, d <= 128)
+  const int r = launch_cand2_leaf<TX>(X, d, ldx, C, v, lab_out, base, nseg,
+                                      dev_info().cus, s);
+  return r == 1 ? fail(DKM_E_ARG, "two-candidate re-check: d % 8 != 0") : r;
 }
 
 template <class TX>

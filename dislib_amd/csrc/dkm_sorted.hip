@@ -33,7 +33,7 @@
 //
 // A tile is handed to k_screen_b2 (tile-list mode) when no row carries a
 // valid label, when a row is not finite / too large for the fp32 bound, or
-// when more than B2_RTHR rows keep more than B2_ENT entries (b2's top-3
+// when more than B2_RTHR rows keep more than SENT entries (b2's top-3
 // pass).  Nothing of such a tile is written here.
 #include <hip/hip_runtime.h>
 
@@ -59,9 +59,13 @@ constexpr int SBS = DKM_AB_SBS;  // threads per block (12 waves: 3 per SIMD)
 #define DKM_AB_SORTED_BSCALE 1
 #endif
 constexpr int SCH = 16;          // consecutive image tiles per chunk
+// kept (score, centre) entries per row besides its hint: up to 1 + SENT
+// candidates go to k_candn's 6-centre list instead of the exhaustive
+// re-check (k_screen_b2 keeps 3)
+constexpr int SENT = 5;
 // per-wave LDS scratch: -T[32], count[32], s_hat_p[32], 2B[32], hint[32],
-// then the kept entries [32][B2_ENT] (score bits, centre)
-constexpr int SS_BYTES = 5 * 128 + 32 * B2_ENT * 8;
+// then the kept entries [32][SENT] (score bits, centre)
+constexpr int SS_BYTES = 5 * 128 + 32 * SENT * 8;
 
 // max of a float over the 32 lanes of each half-wave (both halves hold the
 // same rows): DPP within 16-lane rows, then a 16-lane swap.  The values are
@@ -226,7 +230,7 @@ __global__ void __launch_bounds__(SBS)
       // skipped in the block tests of every row (below)
       const bool seed = minor && sp0 <= T;
       s_cnt[r] = seed ? 1 : 0;
-      if (seed) s_ent[r * B2_ENT] = make_int2(__float_as_int(sp0), p0);
+      if (seed) s_ent[r * SENT] = make_int2(__float_as_int(sp0), p0);
       if (mixed) s_hp[r] = valid ? pr : -1;
     }
     wave_sync();
@@ -323,8 +327,8 @@ __global__ void __launch_bounds__(SBS)
     if (passed) {
       auto push = [&](int row, float s, int j) {
         const int slot = atomicAdd(&s_cnt[row], 1);
-        if (slot < B2_ENT)
-          s_ent[row * B2_ENT + slot] = make_int2(__float_as_int(s), j);
+        if (slot < SENT)
+          s_ent[row * SENT + slot] = make_int2(__float_as_int(s), j);
       };
       int pg[16];
 #pragma unroll
@@ -379,20 +383,20 @@ __global__ void __launch_bounds__(SBS)
       return;
     }
     const float spr = s_sp[r], btr = s_bt[r];
-    float sv[B2_ENT + 1];
-    int cv[B2_ENT + 1];
-    bool ok[B2_ENT + 1];
+    float sv[SENT + 1];
+    int cv[SENT + 1];
+    bool ok[SENT + 1];
     sv[0] = spr;
     cv[0] = pr;
     ok[0] = true;
 #pragma unroll
-    for (int e = 0; e < B2_ENT; ++e) {
-      const int2 en = s_ent[r * B2_ENT + e];
+    for (int e = 0; e < SENT; ++e) {
+      const int2 en = s_ent[r * SENT + e];
       sv[e + 1] = __int_as_float(en.x);
       cv[e + 1] = en.y;
       ok[e + 1] = e < cnt && (unsigned)en.y < (unsigned)k;
     }
-    const bool over = cnt > B2_ENT;
+    const bool over = cnt > SENT;
     const uint64_t mo = __ballot(over && valid && h == 0);
     if (__popcll(mo) > B2_RTHR) {  // b2's top-3 pass takes the tile
       to_fallback(t);
@@ -404,7 +408,7 @@ __global__ void __launch_bounds__(SBS)
     float bs = INFINITY;
     int bc = 0x7fffffff;
 #pragma unroll
-    for (int e = 0; e <= B2_ENT; ++e)
+    for (int e = 0; e <= SENT; ++e)
       if (ok[e] && (sv[e] < bs || (sv[e] == bs && cv[e] < bc))) {
         bs = sv[e];
         bc = cv[e];
@@ -412,7 +416,7 @@ __global__ void __launch_bounds__(SBS)
     int namb = 0, other = 0;
     uint32_t pk[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu};
 #pragma unroll
-    for (int e = 0; e <= B2_ENT; ++e)
+    for (int e = 0; e <= SENT; ++e)
       if (ok[e] && !(sv[e] - bs > btr)) {
 #pragma unroll
         for (int w = 0; w < 6; ++w)
