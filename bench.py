@@ -337,8 +337,8 @@ def screen_products(k, d):
 
 def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
     """Roofline of the assignment call (the dominant kernels).  Small d:
-    HBM-bound, algorithmic bytes = X read (8 d) + labels (delta path:
-    previous label read 4 B + label write 4 B).  d > 128: MFMA-bound, the
+    HBM-bound, algorithmic bytes = the X read (es d per sample, SURVEY
+    8(d)).  d > 128: MFMA-bound, the
     executed MFMA flops of the single-product GEMM screen (2 k d per sample
     over the padded tiles) against the dense bf16 peak.  CSR (C5): the HBM
     bytes of the rows (12 B per stored entry + 8 B of indptr) and labels;
@@ -360,7 +360,10 @@ def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
                              "peak_tbs": L2_PEAK_TBS,
                              "frac": g / sec / 1e12 / L2_PEAK_TBS}}
     elif d <= 128:
-        b = n * (8 * d + 8)
+        # the fit streams X once per iteration, es * d bytes
+        # per sample (the labels the delta path reads and writes are not
+        # counted)
+        b = n * es * d
         ik = r.get("image_kind", 0)
         # bytes the screen actually streams per sample: the resident bf16
         # image (SPLIT: hi + lo, 4 KB per 32-row tile; SINGLE: 1 KB per
@@ -376,7 +379,7 @@ def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
         out = {"bound": "hbm", "achieved": b / sec / 1e9,
                "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": b / sec / 1e9 / HBM_PEAK_GBS,
-               "bytes_per_sample": 8 * d + 8,
+               "bytes_per_sample": es * d,
                "kernel": "dkm_assign_delta / dkm_partial_sum (screen + "
                          "re-check)",
                "kernel_ms": r["kern_ms"],

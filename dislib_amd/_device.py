@@ -12,15 +12,14 @@ per-task pickling of Subsets (reference ``cluster/kmeans/base.py:113-115``,
 for every Lloyd iteration.
 """
 import ctypes
-import os
 
 import numpy as np
 
 from . import _lib
 
-# DKM_X_IMAGE=0: never build the sample image (the screen then converts X
-# itself; identical labels -- A/B and parity runs)
-X_IMAGE = os.environ.get("DKM_X_IMAGE", "1") != "0"
+# False: never build the sample image (the screen then converts X itself;
+# identical labels -- the parity tests switch it through this attribute)
+X_IMAGE = True
 # HBM left free after an image is allocated
 _IMAGE_HEADROOM = 4 << 30
 

@@ -26,8 +26,6 @@ tree).  Extra keyword-only arguments select the assignment arithmetic
 (``mode``: "auto" | "exact" | "screen32" | "bf16x3" | "bf16", identical
 labels) and the device.
 """
-import os
-
 import numpy as np
 from scipy.sparse import csr_matrix, issparse
 
@@ -155,24 +153,17 @@ class KMeans:
 # A refresh is also skipped when no delta since the last one held a
 # nonzero: then no sample changed cluster and the running sums are
 # bit-identical to that last full recomputation.
-REFRESH = int(os.environ.get("DKM_REFRESH", "64"))
+REFRESH = 64
 
 # The fit's label-sorted sample image (dkm_x_image_sorted_*, DESIGN.md
 # 3.11): built from the labels of iteration SORT_AT (the first assignment
-# against centres that are means of samples), it groups each 32-row tile
-# under one label so the single-product screen skips the centre blocks the
-# triangle inequality clears.  Labels are identical without it
-# (DKM_SORTED_IMAGE=0: A/B and parity runs).
-SORTED_IMAGE = os.environ.get("DKM_SORTED_IMAGE", "1") != "0"
+# against centres that are means of samples), together with that
+# iteration's full sums in one pass over X (dkm_x_image_sorted_sums_*); it
+# groups each 32-row tile under one label so the single-product screen skips
+# the centre blocks the triangle inequality clears.  Labels are identical
+# without it (the tests switch it off through this module attribute).
+SORTED_IMAGE = True
 SORT_AT = 1
-# build the sorted image and iteration SORT_AT's sums in one pass over X
-# (dkm_x_image_sorted_sums_*); "0": partial_sum, then the image (A/B runs)
-FUSED_SORT_SUMS = os.environ.get("DKM_FUSED_SORT_SUMS", "1") != "0"
-# A/B knobs of the first two iterations (auto mode): the screen of iteration
-# 0 against the initial centres ("bf16x3" or the single product "bf16"), and
-# whether iteration 1 uses iteration 0's labels as hints ("0": top-3 pass)
-IT0_MODE = os.environ.get("DKM_IT0_MODE", "bf16x3")
-IT1_HINT = os.environ.get("DKM_IT1_HINT", "0") == "1"
 
 
 class _Lloyd:
@@ -227,7 +218,7 @@ class _Lloyd:
         self.mode = _MODES[mode]
         self.tol = tol
         if REFRESH < 1:
-            raise ValueError("DKM_REFRESH must be >= 1, got %d" % REFRESH)
+            raise ValueError("REFRESH must be >= 1, got %d" % REFRESH)
         # every rank must refresh on the same iterations (their delta states
         # are summed): rank 0's setting wins
         self.refresh = _shard.broadcast_int(REFRESH, dd.device)
@@ -263,8 +254,7 @@ class _Lloyd:
             # the first iteration scores against the initial centres, where
             # the single-product screen the library picks for large k x d
             # would leave most samples undecided -- screen it with bf16x3
-            mode = _lib.MODE_BF16X3 if IT0_MODE == "bf16x3" else \
-                _lib.MODE_AUTO | _lib.MODE_NOHINT
+            mode = _lib.MODE_BF16X3
             if self.sorting:
                 image = (None, 0)
         elif self.sorting:
@@ -273,13 +263,12 @@ class _Lloyd:
                 # samples move): the top-3 pass directly, and no image yet
                 # (X is converted in the screen; the sorted image is built
                 # from this iteration's labels)
-                if not IT1_HINT:
-                    mode |= _lib.MODE_NOHINT
+                mode |= _lib.MODE_NOHINT
                 image = (None, 0)
             else:
                 image = self.simg or (None, 0)
         with self._on():
-            if self.sorting and self.it == SORT_AT and FUSED_SORT_SUMS:
+            if self.sorting and self.it == SORT_AT:
                 # labels only, then the sorted image and this iteration's
                 # full sums in one pass over X (iteration 1 always recomputes
                 # in full: _full())
@@ -297,10 +286,6 @@ class _Lloyd:
             else:
                 assign_delta(self.dd, self.C, self.ws, self.labels, self.acc,
                              mode, image=image)
-            if self.sorting and self.it == SORT_AT:
-                simg = sorted_image(self.dd, self.labels[:self.dd.n], self.k,
-                                    self.ws)
-                self.simg = simg if simg[0] is not None else None
 
     def assign(self):
         self.prepare()

@@ -1311,6 +1311,8 @@ __global__ void k_perm_unlabelled(const int32_t *__restrict__ lab, int64_t n,
 // the screen marked -(previous + 2)).  moved != NULL (incremental sums):
 // a synced row whose label differs from its previous one is listed in
 // moved[] (order free; *nmoved counts) and prevs[sample] = previous label.
+// Each lane takes 4 consecutive rows with one 16-B load of plab (4-B loads
+// kept too few bytes in flight: 0.41 ms per C3 sync, 1.2 TB/s).
 __global__ void __launch_bounds__(256)
     k_plab(const int32_t *__restrict__ perm, const int32_t *__restrict__ lab,
            int64_t ntot, int k, int32_t *__restrict__ plab, int only_marked,
@@ -1332,36 +1334,40 @@ __global__ void __launch_bounds__(256)
     wave_sync();
     cnt = 0;
   };
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  // whole waves walk the range together (the ballot below)
-  for (int64_t i0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63ll;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  // whole waves walk the range together (the ballots below); ntot is a
+  // multiple of 32, so a lane's 4 rows are all in range or all out
+  for (int64_t i0 = ((blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~63ll) * 4;
        i0 < ntot; i0 += stride) {
-    const int64_t i = i0 + lane;
-    bool mv = false;
-    int32_t p = -1, old = 0;
-    if (i < ntot) {
-      const int32_t cur = plab[i];
-      if (!only_marked || cur < 0) {
-        p = perm[i];
+    const int64_t i = i0 + 4 * lane;
+    int4 cur4 = make_int4(0, 0, 0, 0);
+    if (i < ntot) cur4 = *(const int4 *)(plab + i);
+    const int32_t cv[4] = {cur4.x, cur4.y, cur4.z, cur4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bool mv = false;
+      int32_t p = -1, old = 0;
+      if (i < ntot && (!only_marked || cv[e] < 0)) {
+        p = perm[i + e];
         const int32_t nw = p >= 0 ? lab[p] : -1;
         // a label outside [0, k) is kept as -1: a negative copy is read as
         // the marker -(previous + 2), and -1 means "no previous label"
-        plab[i] = (unsigned)nw < (unsigned)k ? nw : -1;
-        old = -(cur + 2);
+        plab[i + e] = (unsigned)nw < (unsigned)k ? nw : -1;
+        old = -(cv[e] + 2);
         mv = moved && only_marked && p >= 0 && nw != old;
       }
+      if (!moved) continue;  // kernel-uniform
+      const uint64_t b = __ballot(mv);
+      if (!b) continue;
+      const int c = __popcll(b);
+      if (cnt + c > PLAB_BUF) flush();
+      if (mv) {
+        wb[cnt + lane_prefix(b)] = p;
+        prevs[p] = old;
+      }
+      wave_sync();
+      cnt += c;
     }
-    if (!moved) continue;  // kernel-uniform
-    const uint64_t b = __ballot(mv);
-    if (!b) continue;
-    const int c = __popcll(b);
-    if (cnt + c > PLAB_BUF) flush();
-    if (mv) {
-      wb[cnt + lane_prefix(b)] = p;
-      prevs[p] = old;
-    }
-    wave_sync();
-    cnt += c;
   }
   if (moved && cnt) flush();
 }
@@ -1385,8 +1391,8 @@ int launch_x_image_sorted(const TX *X, int64_t n, int d, int64_t ldx,
   const unsigned g = flat_grid(ntot, cus);
   k_perm_sorted<<<g, 256, 0, s>>>(v.sitems, v.soff + k, n, ntot, perm);
   k_perm_unlabelled<<<g, 256, 0, s>>>(labels, n, k, v.soff + k, cnt, perm);
-  k_plab<<<g, 256, 0, s>>>(perm, labels, ntot, k, im.plab, 0, nullptr,
-                           nullptr, nullptr);
+  k_plab<<<flat_grid((ntot + 3) / 4, cus), 256, 0, s>>>(
+      perm, labels, ntot, k, im.plab, 0, nullptr, nullptr, nullptr);
   if (int r = check_launch("sorted image: permutation")) return r;
   if (!acc) return launch_image_tiles<TX>(X, n, d, ldx, perm, im, cus, s);
   const int64_t nt = (n + 31) / 32;
@@ -1425,7 +1431,7 @@ int launch_plab_sync(const XImage &img, int64_t n, int k, const int32_t *lab,
   const int64_t ntot = (n + 31) / 32 * 32;
   if (moved && hipMemsetAsync(nmoved, 0, 4, s) != hipSuccess)
     return fail(DKM_E_LAUNCH, "sorted image: memset");
-  k_plab<<<flat_grid(ntot, cus), 256, 0, s>>>(img.perm, lab, ntot, k,
+  k_plab<<<flat_grid((ntot + 3) / 4, cus), 256, 0, s>>>(img.perm, lab, ntot, k,
                                               img.plab, 1, moved, nmoved,
                                               prevs);
   return check_launch("sorted image: label sync");

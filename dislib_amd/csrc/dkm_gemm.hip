@@ -467,20 +467,50 @@ __global__ void __launch_bounds__(GTHREADS)
       __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)(G1NRM + w * 128));
   const int64_t tbytes = (int64_t)nks * GSTAGE1;  // one tile, every stage
 
-  auto issue = [&](int q) {  // stage q -> ring buffer q & 3
-    const int m = q / nks, ks = q - m * nks;
+  // The stage stream is issued in order: the tile of the next stage to
+  // issue and its operand bases are kept (wave-uniform, SGPRs) and advanced
+  // per stage, so pair_of's divisions run once per tile, not per stage (as
+  // q / nks plus pair_of per stage they were ~10 SALU per MFMA, C4 PMC).
+  int im = 0, iks = 0, ict = 0;
+  const char *iga = nullptr, *igb = nullptr;
+  auto issue_tile = [&](int m) {
     int st, ct;
     pair_of(lo + j + m * per, st, ct);
-    const char *ga = afrag + ct * tbytes + (int64_t)ks * GSTAGE1;
-    const char *gb = xs + st * tbytes + (int64_t)ks * GSTAGE1;
-    const uint32_t la = lds_base + (uint32_t)((q & (G1RING - 1)) * G1STAGE);
+    st = __builtin_amdgcn_readfirstlane(st);
+    ct = __builtin_amdgcn_readfirstlane(ct);
+    ict = ct;
+    iga = afrag + ct * tbytes;
+    igb = xs + st * tbytes;
+  };
+  issue_tile(0);
+  auto uni = [](const char *p) {  // the compiler cannot prove these uniform
+    const uint64_t a = (uint64_t)p;
+    return (const char *)(((uint64_t)__builtin_amdgcn_readfirstlane(
+                               (uint32_t)(a >> 32))
+                           << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a));
+  };
+  auto issue = [&](int q) {  // stage q (= im nks + iks) -> ring buffer q & 3
+    const char *ga = uni(iga + (int64_t)iks * GSTAGE1);
+    const char *gb = uni(igb + (int64_t)iks * GSTAGE1);
+    const uint32_t la = __builtin_amdgcn_readfirstlane(
+        lds_base + (uint32_t)((q & (G1RING - 1)) * G1STAGE));
     glds16(ga, voff, la);
     glds16(ga, voff2, la + 8192);
     glds16(gb, voff, la + GSTAGE1);
     glds16(gb, voff2, la + GSTAGE1 + 8192);
-    if (ks == 0 && lane < 8)  // the tile's 256 |c|^2: 128 B per wave
-      glds16((const char *)(gcn + (int64_t)ct * GT + w * 32), voffn,
-             nrm_base + (uint32_t)((m & 1) * GT * 4));
+    if (iks == 0 && lane < 8)  // the tile's 256 |c|^2: 128 B per wave
+      glds16(uni((const char *)(gcn + (int64_t)ict * GT + w * 32)), voffn,
+             (uint32_t)__builtin_amdgcn_readfirstlane(
+                 nrm_base + (uint32_t)((im & 1) * GT * 4)));
+    // (readfirstlane: the lane < 8 branch above otherwise makes hipcc keep
+    // the stage counters in VGPRs and the pointers in VGPR pairs)
+    iks = __builtin_amdgcn_readfirstlane(iks + 1);
+    if (iks == nks) {
+      iks = 0;
+      im = __builtin_amdgcn_readfirstlane(im + 1);
+      if (im < ntile) issue_tile(im);
+    }
   };
 
   // accumulators start from |c|^2 of their centre rows (LDS: copied with

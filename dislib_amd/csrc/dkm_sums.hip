@@ -38,6 +38,7 @@ namespace {
 constexpr int SBLK = 1024;    // threads per sort block
 constexpr int SRANGE = 16384; // sort positions per block
 constexpr int SEG = 1024;     // sorted positions per k_seg_sums wave chunk
+constexpr int SEG_LIST = 64;  // the same for moved-sample lists
 constexpr int SUMB = 256;     // threads per k_seg_sums block
 
 int cus() {
@@ -203,7 +204,7 @@ __global__ void __launch_bounds__(SUMB)
     k_seg_sums(const TX *__restrict__ X, int64_t ldx, int d,
                const int32_t *__restrict__ sorted,
                const int32_t *__restrict__ off, int k, double sign,
-               double *__restrict__ acc) {
+               double *__restrict__ acc, int seg) {
   constexpr int R = 64 / G;                 // rows in flight per step
   constexpr int U = NJ >= 8 ? 1 : 8 / NJ;   // steps issued together
   const int64_t n = off[k];  // sorted entries (keys outside [0, k) dropped)
@@ -211,8 +212,8 @@ __global__ void __launch_bounds__(SUMB)
   const int col0 = blockIdx.y * (G * NJ);
   const int64_t wv = (int64_t)blockIdx.x * (SUMB / 64) + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * (SUMB / 64);
-  for (int64_t p0 = wv * SEG; p0 < n; p0 += nw * SEG) {
-    const int64_t p1 = std::min(n, p0 + SEG);
+  for (int64_t p0 = wv * seg; p0 < n; p0 += nw * seg) {
+    const int64_t p1 = std::min(n, p0 + seg);
     // cluster of position p0 + sg: largest c with off[c] <= p0 + sg
     const int64_t q0 = p0 + sg;
     int lo_c = 0, hi_c = k;  // off[lo_c] <= q0 < off[hi_c]
@@ -280,8 +281,12 @@ template <class TX>
 static int launch_seg(const TX *X, int64_t ldx, int d, const int32_t *sorted,
                       int64_t nh, const int32_t *off, int k, double sign,
                       double *acc, hipStream_t s, bool list = false) {
-  const int64_t chunks = (nh + SEG - 1) / SEG;
-  // explicit (moved-sample) lists: a smaller grid, grid-striding
+  // explicit (moved-sample) lists: a smaller grid, grid-striding, and short
+  // wave chunks -- the list is usually far shorter than its bound nh, and a
+  // 1024-position chunk per wave left a 100k-row list to ~100 waves, each
+  // with two dependent loads per step (1 ms per C3 delta pass)
+  const int seg = list ? SEG_LIST : SEG;
+  const int64_t chunks = (nh + seg - 1) / seg;
   const int64_t g = std::max<int64_t>(
       1, std::min<int64_t>((int64_t)cus() * (list ? 2 : 8),
                            (chunks + SUMB / 64 - 1) / (SUMB / 64)));
@@ -289,7 +294,7 @@ static int launch_seg(const TX *X, int64_t ldx, int d, const int32_t *sorted,
   {                                                                           \
     const unsigned gy = (unsigned)((d + GG * NN - 1) / (GG * NN));            \
     k_seg_sums<TX, GG, NN><<<dim3((unsigned)g, gy), SUMB, 0, s>>>(            \
-        X, ldx, d, sorted, off, k, sign, acc);                                \
+        X, ldx, d, sorted, off, k, sign, acc, seg);                           \
   }
   if (d <= 8) DKM_SEG(8, 1)
   else if (d <= 16) DKM_SEG(16, 1)

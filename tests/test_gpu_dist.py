@@ -7,7 +7,7 @@
   the CUDA buffers), each fitting its shard with the HIP kernels, against
   the oracle on the whole dataset -- labels bit-exact, centres within 1e-9,
   n_iter, the delta/refresh state kept consistent across ranks (rank 0's
-  DKM_REFRESH wins) and ``random_state=None`` (rank 0's draw is used).
+  REFRESH wins) and ``random_state=None`` (rank 0's draw is used).
 """
 import ctypes
 import os

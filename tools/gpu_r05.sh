@@ -5,6 +5,7 @@
 #   t_all     the whole GPU suite
 #   diag      tools/c3_diag.py on the main library and on libdkm_old.so
 #   c3it      C3 bench line under a rocprofv3 kernel trace, per iteration
+#   c4it      C4 bench line under a rocprofv3 kernel trace, per iteration
 #   c3ab      C3 bench line, main vs libdkm_old.so, two rounds
 #   bench     default bench.py
 TAG=${1:-r05}; shift
@@ -21,6 +22,7 @@ step() {  # name limit cmd...
 }
 PT="python -u -m pytest -p no:cacheprovider --timeout 200 --timeout-method thread -q"
 C3="python bench.py --n 125000000 --d 64 --k 1000 --steps 8 --warmup 2 --no-cpu --only-headline"
+C4="python bench.py --n 10000000 --d 1024 --k 4096 --steps 3 --warmup 1 --no-cpu --only-headline"
 OLD=$PWD/dislib_amd/libdkm_old.so
 for s in "$@"; do
   case $s in
@@ -34,6 +36,10 @@ for s in "$@"; do
       [ -n "$DB" ] && python tools/prof_iters.py $DB > $P/iters.txt 2>&1 && rm -f $DB
       find $P -type f ! -name 'iters.txt' ! -name '*kernel_stats.csv' -delete
       cut -c1-300 $P/iters.txt ;;
+    c4it) P=$OUT/${TAG}_c4it; mkdir -p $P
+      step c4it 400 rocprofv3 --kernel-trace --stats -d $P -o run -- $C4
+      DB=$(find $P -name "*.db" | head -1); [ -n "$DB" ] && python tools/prof_iters.py $DB > $P/iters.txt 2>&1 && rm -f $DB; find $P -type f ! -name iters.txt -delete
+      cut -c1-400 $P/iters.txt ;;
     c3ab) for r in 1 2; do for v in main old; do
         if [ $v = old ]; then export DKM_LIB=$OLD; else unset DKM_LIB; fi
         step c3_$v$r 300 $C3
