@@ -644,6 +644,10 @@ __global__ void __launch_bounds__(GTHREADS)
     load_sub(q0, 0, A0, B0);
     load_sub(q0, 1, A1, B1);
     mfmas(A0, B0);
+    // (Pinning this order with sched_barrier -- reads strictly before the
+    // MFMAs that cover them -- made the bare loop 3 % faster but the whole
+    // kernel 6-9 % slower on one box, A/B r05n: hipcc's interleaving of the
+    // ring copies and reads with the MFMAs is kept.)
     for (int ks = 1; ks < nks; ++ks) {
       sync_issue(q0 + ks);
       load_sub(q0 + ks, 0, A0, B0);

@@ -49,29 +49,44 @@ typedef const __attribute__((address_space(4))) double cdouble;
 // ---------------------------------------------------------------------------
 // kNN
 // ---------------------------------------------------------------------------
+// Ranking key of a squared distance r >= 0: its bit pattern (monotonic for
+// non-negative doubles; -0.0 folded onto +0.0), NaN after +inf as sklearn's
+// argpartition ranks it (data overflowing to inf - inf), and the empty slot
+// after every real row, so every list fills with real rows.
+constexpr uint64_t KEY_NAN = 0x7ff8000000000000ull;
+constexpr uint64_t KEY_EMPTY = ~0ull;
+__device__ __forceinline__ uint64_t rkey(double r) {
+  return r != r ? KEY_NAN : (uint64_t)__double_as_longlong(r + 0.0);
+}
+__device__ __forceinline__ double key_r(uint64_t key) {
+  return key == KEY_EMPTY ? INFINITY : __longlong_as_double((long long)key);
+}
+
 template <int K>
 struct TopK {
-  double r[K];
+  uint64_t r[K];
   int i[K];
   __device__ __forceinline__ void init() {
 #pragma unroll
     for (int s = 0; s < K; ++s) {
-      r[s] = INFINITY;
+      r[s] = KEY_EMPTY;
       i[s] = INT32_MAX;
     }
   }
-  // (v, j) by lexicographic (r, index).  The comparison stays lexicographic
-  // for the entry carried down the list after a swap: a displaced (r, i)
-  // must still go ahead of a held (r, i') with i < i' (a "strict <, empty
-  // slots take ties" rule for scan-order pushes drops it instead).  An empty
-  // slot (+inf, INT32_MAX) also takes a row at +inf (overflowed distance),
-  // so every list fills with real rows (sklearn returns them too).
-  __device__ __forceinline__ void push(double v, int j) {
-    if (v < r[K - 1] || (v == r[K - 1] && j < i[K - 1])) {
+  // (v, j) by lexicographic (key, index).  The comparison stays
+  // lexicographic for the entry carried down the list after a swap: a
+  // displaced (r, i) must still go ahead of a held (r, i') with i < i' (a
+  // "strict <, empty slots take ties" rule for scan-order pushes drops it
+  // instead).
+  __device__ __forceinline__ bool before_last(uint64_t v, int j) const {
+    return v < r[K - 1] || (v == r[K - 1] && j < i[K - 1]);
+  }
+  __device__ __forceinline__ void push(uint64_t v, int j) {
+    if (before_last(v, j)) {
 #pragma unroll
       for (int s = 0; s < K; ++s) {
         const bool lt = v < r[s] || (v == r[s] && j < i[s]);
-        const double tr = r[s];
+        const uint64_t tr = r[s];
         const int ti = i[s];
         r[s] = lt ? v : tr;
         i[s] = lt ? j : ti;
@@ -131,24 +146,23 @@ __global__ void __launch_bounds__(NB)
   cdouble *xc = (cdouble *)X;
   if (flr) {
     // a later pass: only (r, j) strictly after the previous pass's last
-    const double fr = live ? flr[q] : INFINITY;
+    const uint64_t fr = live ? (uint64_t)__double_as_longlong(flr[q])
+                             : KEY_EMPTY;
     const int fi = live ? fli[q] : INT32_MAX;
     for (int64_t j = j0; j < j1; ++j) {
-      const double r = seq_r<MAXD>(qv, qrow, xc + j * ldx, d);
+      const uint64_t r = rkey(seq_r<MAXD>(qv, qrow, xc + j * ldx, d));
       if (r > fr || (r == fr && (int)j > fi)) top.push(r, (int)j);
     }
   } else {
-    for (int64_t j = j0; j < j1; ++j) {
-      const double r = seq_r<MAXD>(qv, qrow, xc + j * ldx, d);
-      top.push(r, (int)j);
-    }
+    for (int64_t j = j0; j < j1; ++j)
+      top.push(rkey(seq_r<MAXD>(qv, qrow, xc + j * ldx, d)), (int)j);
   }
   if (!live) return;
   double *po = pr + (q * P + p) * K;
   int *io = pi + (q * P + p) * K;
 #pragma unroll
-  for (int s = 0; s < K; ++s) {
-    po[s] = top.r[s];
+  for (int s = 0; s < K; ++s) {  // keys, as bits in the partial buffer
+    po[s] = __longlong_as_double((long long)top.r[s]);
     io[s] = top.i[s];
   }
 }
@@ -186,7 +200,8 @@ __global__ void __launch_bounds__(NB)
     const double v = qd[t];
     xx += v * v;
   }
-  const double fr = (live && flr) ? flr[q] : -INFINITY;
+  const uint64_t fr =
+      (live && flr) ? (uint64_t)__double_as_longlong(flr[q]) : 0;
   const int fi = (live && fli) ? fli[q] : -1;
   TopK<K> top;
   top.init();
@@ -216,15 +231,18 @@ __global__ void __launch_bounds__(NB)
     } else {
       r = r < 0.0 ? 0.0 : r;
     }
-    // a later pass: only (r, j) strictly after the previous pass's last
-    if (r > fr || (r == fr && (int)j > fi)) top.push(r, (int)j);
+    // (finite data whose squares overflow: inf - inf = NaN, ranked after
+    // +inf).  A later pass: only (r, j) strictly after the previous pass's
+    // last.
+    const uint64_t rk = rkey(r);
+    if (rk > fr || (rk == fr && (int)j > fi)) top.push(rk, (int)j);
   }
   if (!live) return;
   double *po = pr + (q * P + p) * K;
   int *io = pi + (q * P + p) * K;
 #pragma unroll
   for (int s = 0; s < K; ++s) {
-    po[s] = top.r[s];
+    po[s] = __longlong_as_double((long long)top.r[s]);
     io[s] = top.i[s];
   }
 }
@@ -243,8 +261,8 @@ __global__ void __launch_bounds__(NB)
     const double *a = pr + (q * P + p) * K;
     const int *b = pi + (q * P + p) * K;
     for (int s = 0; s < kn; ++s) {
-      const double v = a[s];
-      if (!(v < top.r[K - 1]) && !(v == top.r[K - 1] && b[s] < top.i[K - 1]))
+      const uint64_t v = (uint64_t)__double_as_longlong(a[s]);
+      if (!top.before_last(v, b[s]))
         break;  // the partition's list is sorted: nothing further enters
       top.push(v, b[s]);
     }
@@ -252,12 +270,12 @@ __global__ void __launch_bounds__(NB)
 #pragma unroll
   for (int s = 0; s < K; ++s)
     if (s < kn) {
+      const double r = key_r(top.r[s]);
       // f32: r is a float32 value; the fp64 sqrt rounds to float32's own
-      out_d[q * ldo + s] = f32 ? (double)(float)sqrt(top.r[s])
-                               : sqrt(top.r[s]);
+      out_d[q * ldo + s] = f32 ? (double)(float)sqrt(r) : sqrt(r);
       out_i[q * ldo + s] = (int64_t)top.i[s];
-      if (s == kn - 1) {  // where the next pass starts
-        flr[q] = top.r[s];
+      if (s == kn - 1) {  // where the next pass starts (a key)
+        flr[q] = __longlong_as_double((long long)top.r[s]);
         fli[q] = top.i[s];
       }
     }

@@ -121,6 +121,28 @@ def test_kneighbors_overflowed_distances_fill_the_list():
         assert len(set(row.tolist())) == 8
 
 
+def test_sparse_kneighbors_nan_distances_rank_last():
+    """Finite data whose squares overflow: r = -2 inf + inf + inf = NaN.
+    NaN ranks after +inf (numpy's argpartition / argsort order, which the
+    reference's sklearn brute force uses), and such rows fill the list as
+    real fit indices, never the INT32_MAX empty-slot sentinel."""
+    import scipy.sparse as sp
+    fd = np.zeros((6, 3))
+    fd[0, 0] = 1e200            # with the query: inf - inf = NaN
+    fd[1:, 1] = np.arange(1, 6)
+    qd = np.zeros((2, 3))
+    qd[:, 0] = 1e200
+    mf, mq = sp.csr_matrix(fd), sp.csr_matrix(qd)
+    gd, gi = _knn_csr(mf, mq, 6, 6, 2)
+    f = (mf.indptr.astype(np.int64), mf.indices, mf.data)
+    q = (mq.indptr.astype(np.int64), mq.indices, mq.data)
+    od, oi = orc.kneighbors_csr(f, q, 6)
+    assert np.array_equal(gi, oi)
+    assert np.array_equal(gd, od, equal_nan=True)
+    assert gi[:, -1].tolist() == [0, 0] and np.isnan(gd[:, -1]).all()
+    assert np.isinf(gd[:, :-1]).all()
+
+
 def test_kneighbors_return_indices_only_and_device_data():
     from dislib_amd.data import load_data
     from dislib_amd.neighbors import NearestNeighbors

@@ -4,7 +4,7 @@
                              [--centres data|init] [--f32]
 
 Reports ms per dkm_partial_sum call, the executed bf16 MFMA rate
-(3 products x 2 k dpad flops per sample) against the 2.5 PF dense peak, and
+(3 products, or 1 with --mode bf16, x 2 k dpad flops per sample) against the 2.5 PF dense peak, and
 the number of samples sent to the exact paths.
 """
 import argparse
@@ -26,6 +26,7 @@ def main():
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--centres", default="data", choices=["data", "init"])
     p.add_argument("--f32", action="store_true")
+    p.add_argument("--mode", default="bf16x3", choices=["bf16x3", "bf16"])
     p.add_argument("--kind", default="partial",
                    choices=["partial", "predict", "delta"])
     a = p.parse_args()
@@ -51,7 +52,7 @@ def main():
     ws = _device.Workspace(k, d, n, dev)
     acc = torch.zeros(k * (d + 1), dtype=torch.float64, device=dev)
     lab = torch.full((n,), -1, dtype=torch.int32, device=dev)
-    m = _lib.MODE_BF16X3
+    m = _lib.MODE_BF16X3 if a.mode == "bf16x3" else _lib.MODE_BF16
     times = []
     for r in range(a.reps + 1):
         _device.prepare(C, ws, acc)
@@ -69,7 +70,7 @@ def main():
     ms = 1e3 * float(np.median(times))
     dpad = (d + 31) // 32 * 32
     kpad = (k + 255) // 256 * 256
-    flops = 6.0 * n * kpad * dpad
+    flops = (6.0 if a.mode == "bf16x3" else 2.0) * n * kpad * dpad
     out = {"n": n, "d": d, "k": k, "kind": a.kind, "f32": a.f32,
            "centres": a.centres, "ms": ms, "ms_all": [1e3 * t for t in times],
            "bf16_tflops": flops / ms * 1e-9,
