@@ -114,9 +114,9 @@ struct WsView {
   float *cn32;    // k fp32 ||c||^2 (computed in fp64, rounded once)
   double *cn64;   // k fp64 ||c||^2, sequential over t (sklearn row_norms)
   double *ct64;   // d x ct_ld(k) transposed centres (exact re-checks, CSR)
-  float *ct32;    // fp32 transposed centres of the CSR screen, sliced:
+  uint16_t *ctb;  // bf16 transposed centres of the CSR screen, sliced:
                   // slice s = d rows of csr_slice_width(k, d) centres,
-                  // contiguous (csr_ct32_len floats in all)
+                  // contiguous (csr_ctb_len values in all)
   float *cfrag;   // fp32 -2*centres in MFMA A-fragment order (dkm_dense)
   float *cnpad;   // kpad16 fp32 ||c||^2, 2^100 for padding centres
   uint16_t *bfrag; // bf16 hi/lo of -2*centres, 16x16x32 fragment order
@@ -258,20 +258,20 @@ constexpr int TL_CAP = 2048;
 constexpr int TL_SEGS = 8192;
 
 // CSR screen (dkm_sparse.hip): the centres are cut into S slices (a power
-// of two <= 8) whose fp32 C^T fits CSR_SLICE_BYTES, never narrower than one
-// 32-centre pass; slice s is stored as its own contiguous d x width block,
+// of two <= 8) whose bf16 C^T fits CSR_SLICE_BYTES, never narrower than one
+// 64-centre pass; slice s is stored as its own contiguous d x width block,
 // so that the lines of a slice spread over every set of an XCD's L2 (rows
 // of the full d x k transpose, 1 KB apart at k = 256, fell into one set in
 // eight: 10 % L2 misses at C5, profiles/r04/pmc/c5_csr_pmc_summary_4M.txt).
 // 16 MB: every slice costs a walk over the entries, which outweighs the L2
 // locality of smaller slices (C5's 10 MB table: one slice is fastest).
 constexpr size_t CSR_SLICE_BYTES = 16u << 20;
-constexpr int CSR_PASS = 32;
+constexpr int CSR_PASS = 64;
 __host__ __device__ inline int csr_slices(int64_t k, int64_t d) {
   int S = 1;
   while (S < 8 && (k + S - 1) / S > CSR_PASS &&
          (size_t)(((k + S - 1) / S + CSR_PASS - 1) / CSR_PASS * CSR_PASS * d *
-                  4) > CSR_SLICE_BYTES)
+                  2) > CSR_SLICE_BYTES)
     S *= 2;
   return S;
 }
@@ -279,7 +279,7 @@ __host__ __device__ inline int64_t csr_slice_width(int64_t k, int64_t d) {
   const int S = csr_slices(k, d);
   return ((k + S - 1) / S + CSR_PASS - 1) / CSR_PASS * CSR_PASS;
 }
-__host__ __device__ inline int64_t csr_ct32_len(int64_t k, int64_t d) {
+__host__ __device__ inline int64_t csr_ctb_len(int64_t k, int64_t d) {
   return (int64_t)csr_slices(k, d) * csr_slice_width(k, d) * d;
 }
 

@@ -15,23 +15,26 @@
 // labelled by the screen below only when a rigorous bound proves the
 // reference arithmetic picks the same centre, otherwise by that arithmetic.
 //
-// The time goes into gathering nnz rows of C^T per sample (k values each:
-// 10 KB in fp32 at C5, k = 256, 10 nnz).  Large tables are cut into S
-// slices (S = 1, 2, 4 or 8; CSR_SLICE_BYTES) and block b works on slice
-// b % S, so blocks b and b + 8 share an XCD and gather from one slice (a
-// speed assumption, never a correctness one).  Every slice costs a walk
-// over the sample's entries, a reduction and a state per sample, and that
-// costs more than the L2 locality gains: at C5 the 10 MB table runs as ONE
-// slice (S = 1: 7.0 ms per step; S = 2: 7.3, S = 4: 7.6, S = 8 (4 MB-L2
-// slices): 8.8; profiles/r04/c5ab).
-//   k_csr_screen   8 lanes per sample (8 samples per wave), 4 centres per
-//                  lane per 32-centre pass, 16-B loads of the fp32 C^T
-//                  (d x ct_ld(k)); the row's entries staged 8 at a time in
-//                  the group's lanes and walked by ds_bpermute.  Per centre
-//                  j only s_j = |c_j|^2 - 2 x.c_j (one fp32 fma per stored
-//                  entry); the slice's state is its two smallest scores and
-//                  the index of the first; the bound B (below) is one per
-//                  sample.
+// The time goes into gathering nnz rows of C^T per sample (k values each),
+// an L2-bandwidth-bound walk: at C5 (k = 256, 10 nnz) the fp32 table was
+// 10 KB per sample from a 10.24 MB table that overflows an XCD's 4 MB L2
+// (16 TB/s of L2 gathers, 3.4 KB/sample of fabric traffic, round 4).  The
+// screen table is therefore bf16 (round to nearest from fp64; the bound
+// below widens by the rounding): half the bytes per gather and a 5.12 MB
+// table whose L2 share doubles.  Large tables are cut into S slices (S = 1,
+// 2, 4 or 8; CSR_SLICE_BYTES) and block b works on slice b % S, so blocks b
+// and b + 8 share an XCD and gather from one slice (a speed assumption,
+// never a correctness one).  Every slice costs a walk over the sample's
+// entries, a reduction and a state per sample, and that costs more than the
+// L2 locality gains (fp32 C5: S = 1 7.0 ms per step; S = 2: 7.3, S = 4: 7.6,
+// S = 8: 8.8; profiles/r04/c5ab).
+//   k_csr_screen   8 lanes per sample (8 samples per wave), 8 centres per
+//                  lane per 64-centre pass, 16-B loads of the bf16 C^T; the
+//                  row's entries staged 8 at a time in the group's lanes and
+//                  walked by ds_bpermute.  Per centre j only s_j = |c_j|^2 -
+//                  2 x.c_j (one fp32 fma per stored entry); the slice's
+//                  state is its two smallest scores and the index of the
+//                  first; the bound B (below) is one per sample.
 //   k_csr_merge    one lane per sample: the slices' states merged (ascending
 //                  centre ranges: a strict < keeps the first index); decided
 //                  when s1 + B < s2 - B for the best s1 and the next s2 --
@@ -49,10 +52,11 @@
 // Samples are processed in chunks so that the S slice states fit the
 // workspace tail (20 bytes per slice and sample).
 //
-// The bound.  With u = 2^-24 (fp32) and w = 2^-53 (fp64), n stored entries,
-// A_j >= sum |x_v c_jv| and M_j = xx + |c_j|^2 + 2 A_j + |s_j| >= the
-// magnitude of every partial result:
-//   fp32 dot vs exact          (n + 2) u A_j     (inputs rounded, fma chain)
+// The bound.  With u = 2^-24 (fp32), w = 2^-53 (fp64) and b = 2^-9 (bf16,
+// round to nearest), n stored entries, A_j >= sum |x_v c_jv| and M_j = xx +
+// |c_j|^2 + 2 A_j + |s_j| >= the magnitude of every partial result:
+//   bf16 table vs exact        b (1 + 2^-14) A_j (c_jv rounded to bf16)
+//   fp32 dot vs exact          (n + 2) u A_j     (x rounded, fma chain)
 //   sklearn's fp64 dot         n w A_j
 //   s_j rounding, |c|^2 -> fp32  u |s_j| + u |c_j|^2
 //   sklearn's two additions    2 w M_j;  sqrt strictly monotone: 4 w M_j
@@ -80,7 +84,8 @@ namespace {
 constexpr int CSR_BLOCK = 256;
 constexpr int CSR_G = 8;                   // lanes per sample
 constexpr int CSR_SPW = WAVE / CSR_G;      // samples per wave
-static_assert(CSR_PASS == 4 * CSR_G, "a pass is 4 centres per lane");
+constexpr int CSR_W = 8;                   // centres per lane and pass
+static_assert(CSR_PASS == CSR_W * CSR_G, "a pass is 8 centres per lane");
 constexpr int CSR_SEGP = 4096;             // sorted positions per sums block
 constexpr int CSR_TD = 16384;              // sums columns per LDS tile
 constexpr int CSR_SUMB = 1024;
@@ -109,9 +114,9 @@ __device__ __forceinline__ void add_row(const int64_t *indptr,
 
 }  // namespace
 
-// NP passes of 32 centres per walk over the entries (a slice wider than
-// 32 * NP centres is walked again).  Slice s covers centres
-// [s * ks, min(k, (s + 1) * ks)), ks a multiple of 32.  Per centre only the
+// NP passes of 64 centres per walk over the entries (a slice wider than
+// 64 * NP centres is walked again).  Slice s covers centres
+// [s * ks, min(k, (s + 1) * ks)), ks a multiple of 64.  Per centre only the
 // fp32 score s_j = |c_j|^2 - 2 x.c_j (one fma per stored entry); the bound
 // B is one per sample (the header comment), so a lane keeps its two
 // smallest scores and the index of the smallest.
@@ -120,7 +125,7 @@ __global__ void __launch_bounds__(CSR_BLOCK)
     k_csr_screen(const int64_t *__restrict__ indptr,
                  const int32_t *__restrict__ indices,
                  const double *__restrict__ data, int64_t i0, int64_t m,
-                 const float *__restrict__ CT, int64_t dct,
+                 const uint16_t *__restrict__ CT, int64_t dct,
                  const float *__restrict__ cn, int k, int S, int ks,
                  const WsHeader *__restrict__ hdr,
                  SliceState *__restrict__ pst, int32_t *__restrict__ pidx,
@@ -132,8 +137,8 @@ __global__ void __launch_bounds__(CSR_BLOCK)
   const int64_t wv = stream * (CSR_BLOCK / 64) + (threadIdx.x >> 6);
   const int64_t nwv = nstream * (CSR_BLOCK / 64);
   const int j_lo = s * ks, j_hi = min(k, j_lo + ks);
-  // this slice's d x ks block of the sliced fp32 C^T
-  const float *CTs = CT + (int64_t)s * dct * ks - j_lo;
+  // this slice's d x ks block of the sliced bf16 C^T
+  const uint16_t *CTs = CT + (int64_t)s * dct * ks - j_lo;
   // max_j ||c_j|| (fp64, ordered bits), rounded up to fp32
   const float cmax =
       (float)__longlong_as_double((long long)hdr->cmax_bits) * 1.000001f;
@@ -175,19 +180,19 @@ __global__ void __launch_bounds__(CSR_BLOCK)
     int i1 = 0x7fffffff;
     float xx = 0.f;
     for (int jp = j_lo; jp < j_hi; jp += CSR_PASS * NP) {
-      float dot[NP][4];
+      float dot[NP][CSR_W];
 #pragma unroll
       for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int h = 0; h < 4; ++h) dot[p][h] = 0.f;
+        for (int h = 0; h < CSR_W; ++h) dot[p][h] = 0.f;
       const bool first = jp == j_lo;
       // the pass's |c_j|^2 load early (used after the gathers)
-      float cnv[NP][4];
+      float cnv[NP][CSR_W];
 #pragma unroll
       for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const int j = jp + CSR_PASS * p + 4 * gl + h;
+        for (int h = 0; h < CSR_W; ++h) {
+          const int j = jp + CSR_PASS * p + CSR_W * gl + h;
           cnv[p][h] = j < j_hi ? cn[j] : 0.f;
         }
       for (int64_t c0 = a; c0 < b; c0 += CSR_G) {
@@ -212,20 +217,21 @@ __global__ void __launch_bounds__(CSR_BLOCK)
         constexpr int EM = NP >= 4 ? 2 : CSR_G;
         auto chunk = [&](auto e_tag, int h) {
           constexpr int E = decltype(e_tag)::value;
-          float4 cv[E][NP];
+          uint4 cv[E][NP];
           float vv[E];
 #pragma unroll
           for (int e = 0; e < E; ++e) {
             const int idx = __shfl(myi, gbase + h + e, WAVE);
             vv[e] = __shfl(myv, gbase + h + e, WAVE);
-            // byte offset < 2^32: d x ks floats per slice (csr_run checks)
-            const float *row = (const float *)(
-                (const char *)CTs + 4u * (uint32_t)(idx * ks + jp + 4 * gl));
+            // byte offset < 2^32: d x ks bf16 per slice (csr_run checks)
+            const uint16_t *row = (const uint16_t *)(
+                (const char *)CTs +
+                2u * (uint32_t)(idx * ks + jp + CSR_W * gl));
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
               const bool blk = p == 0 || jp + CSR_PASS * p < j_hi;
-              cv[e][p] = blk ? *(const float4 *)(row + CSR_PASS * p)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+              cv[e][p] = blk ? *(const uint4 *)(row + CSR_PASS * p)
+                             : make_uint4(0u, 0u, 0u, 0u);
             }
           }
 #pragma unroll
@@ -234,10 +240,15 @@ __global__ void __launch_bounds__(CSR_BLOCK)
             if (first) xx = fmaf(v, v, xx);
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
-              dot[p][0] = fmaf(v, cv[e][p].x, dot[p][0]);
-              dot[p][1] = fmaf(v, cv[e][p].y, dot[p][1]);
-              dot[p][2] = fmaf(v, cv[e][p].z, dot[p][2]);
-              dot[p][3] = fmaf(v, cv[e][p].w, dot[p][3]);
+              const uint32_t w4[4] = {cv[e][p].x, cv[e][p].y, cv[e][p].z,
+                                      cv[e][p].w};
+#pragma unroll
+              for (int t = 0; t < 4; ++t) {  // bf16 pair -> two fp32
+                dot[p][2 * t] =
+                    fmaf(v, __uint_as_float(w4[t] << 16), dot[p][2 * t]);
+                dot[p][2 * t + 1] = fmaf(
+                    v, __uint_as_float(w4[t] & 0xffff0000u), dot[p][2 * t + 1]);
+              }
             }
           }
         };
@@ -253,8 +264,8 @@ __global__ void __launch_bounds__(CSR_BLOCK)
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const int j = jp + CSR_PASS * p + 4 * gl + h;
+        for (int h = 0; h < CSR_W; ++h) {
+          const int j = jp + CSR_PASS * p + CSR_W * gl + h;
           if (j < j_hi) {  // centres ascending per lane: strict < = first
             const float sj = fmaf(-2.f, dot[p][h], cnv[p][h]);
             if (sj < s1) {
@@ -288,12 +299,13 @@ __global__ void __launch_bounds__(CSR_BLOCK)
         // the bound of every centre of the sample (header comment): A >=
         // sum |x_v c_jv| by Cauchy-Schwarz, |c_j|^2 <= cmax^2, |s_j| <=
         // |c_j|^2 + 2A; doubled, + 2^-100 for underflow; NaN / inf: no
-        // decision
+        // decision.  The bf16 table: 2 x (2 x b A) = 2^-7 A (1 + 2^-14).
         const float xx_up = xx * (1.f + (nf + 4.f) * 0x1.0p-23f);
         const float A = sqrtf(xx_up) * cmax * (1.f + 0x1.0p-20f);
         const float c2 = cmax * cmax * (1.f + 0x1.0p-22f);
         const float M = xx_up + 2.f * c2 + 4.f * A;
-        const float B = (0x1.0p-23f * (2.f * c2 + 2.f * A +
+        const float B = (0x1.0p-7f * (1.f + 0x1.0p-14f) * A +
+                         0x1.0p-23f * (2.f * c2 + 2.f * A +
                                        2.f * (nf + 2.f) * A) +
                          (2.f * nf + 6.f) * 0x1.0p-52f * M + 0x1.0p-100f) *
                         (1.f + 0x1.0p-20f);
@@ -528,7 +540,7 @@ static int csr_run(const int64_t *indptr, const int32_t *indices,
     op = OP_FULL_ATOMIC;  // no label array to sort (or k beyond the sort)
   const int S = csr_slices(k, d);
   const int ks = (int)csr_slice_width(k, d);
-  if ((uint64_t)d * (uint64_t)ks * 4 > 0xffffffffull)  // 32-bit gather offsets
+  if ((uint64_t)d * (uint64_t)ks * 2 > 0xffffffffull)  // 32-bit gather offsets
     return fail(DKM_E_ARG, std::string(who) + ": d x slice width beyond 4 GiB");
   // per chunk sample: S slice states (12 B), x.x and B bounds (8 B), list
   // slot (4 B)
@@ -555,7 +567,8 @@ static int csr_run(const int64_t *indptr, const int32_t *indices,
     const unsigned g = (unsigned)(per_slice * S);
 #define DKM_SCREEN(NP)                                                       \
   k_csr_screen<NP><<<g, CSR_BLOCK, 0, st>>>(indptr, indices, data, i0, m,   \
-                                            v.ct32, d, v.cn32,              \
+                                            v.ctb, d,                       \
+                                            v.cn32,                         \
                                             (int)k, S, ks, v.hdr, pst,      \
                                             pidx, pxx, pb)
     if (npass >= 4)

@@ -206,7 +206,9 @@ __global__ void __launch_bounds__(SUMB)
                const int32_t *__restrict__ off, int k, double sign,
                double *__restrict__ acc, int seg) {
   constexpr int R = 64 / G;                 // rows in flight per step
-  constexpr int U = NJ >= 8 ? 1 : 8 / NJ;   // steps issued together
+  // steps issued together: >= 8 loads per lane in flight, and fp32 rows
+  // twice as many (the same bytes in flight as fp64)
+  constexpr int U = (NJ >= 8 ? 1 : 8 / NJ) * (sizeof(TX) == 4 ? 2 : 1);
   const int64_t n = off[k];  // sorted entries (keys outside [0, k) dropped)
   const int lane = threadIdx.x & 63, sg = lane / G, gl = lane % G;
   const int col0 = blockIdx.y * (G * NJ);
@@ -246,12 +248,19 @@ __global__ void __launch_bounds__(SUMB)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t pos = q + (int64_t)u * R;
-        const int32_t it = pos < p1 ? sorted[pos] : -1;
-        const TX *row = X + (int64_t)(it < 0 ? 0 : it) * ldx;
+        const int32_t it = sorted[pos < p1 ? pos : p1 - 1];
+        const TX *row = X + (int64_t)it * ldx;
+        // Unconditional loads from a clamped position / column and no select: a
+        // select of a load lets hipcc branch around each load with a
+        // vmcnt(0) inside (16 serialised loads per row; it did so for fp32,
+        // 1.4 TB/s against 6.0 for fp64, tools/bench_sums.py r05o, and for
+        // fp64 once the address was clamped).  The values of rows past the
+        // chunk and columns past d are never added (pos < p1 below) or
+        // flushed (t < d).
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int t = col0 + gl + G * j;
-          x[u][j] = (it >= 0 && t < d) ? (double)row[t] : 0.0;
+          x[u][j] = (double)row[t < d ? t : d - 1];
         }
       }
 #pragma unroll

@@ -56,7 +56,7 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
   b += round_up(k * 4, 256);          // cn32
   b += round_up(k * 8, 256);          // cn64
   b += round_up(ct_ld(k) * d * 8, 256);  // ct64 (d x ct_ld(k))
-  b += round_up(csr_ct32_len(k, d) * 4, 256);  // ct32 (sliced)
+  b += round_up(csr_ctb_len(k, d) * 2, 256);  // ctb (sliced bf16)
   b += round_up(kpad16(k) * dpad32(d) * 4, 256);  // cfrag
   b += round_up(kpad16(k) * 4, 256);  // cnpad
   b += round_up(kpad16(k) * dpad32(d) * 4, 256);  // bfrag (hi + lo bf16)
@@ -92,8 +92,8 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   p += round_up(k * 8, 256);
   v->ct64 = (double *)p;
   p += round_up(ct_ld(k) * d * 8, 256);
-  v->ct32 = (float *)p;
-  p += round_up(csr_ct32_len(k, d) * 4, 256);
+  v->ctb = (uint16_t *)p;
+  p += round_up(csr_ctb_len(k, d) * 2, 256);
   v->cfrag = (float *)p;
   p += round_up(kpad16(k) * dpad32(d) * 4, 256);
   v->cnpad = (float *)p;
@@ -204,15 +204,17 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ C,
   const int64_t c = blockIdx.x;
   const double *row = C + c * d;
   const int64_t ld = ct_ld(k);
-  // the CSR screen's sliced fp32 C^T: slice c / w, column c % w
+  // the CSR screen's sliced bf16 C^T: slice c / w, column c % w; round to
+  // nearest (fp64 -> fp32 -> bf16: within 2^-9 (1 + 2^-14) relative, the
+  // bound's term)
   const int64_t w = csr_slice_width(k, d);
-  float *ct32s = v.ct32 + (c / w) * d * w + (c % w);
+  uint16_t *ctbs = v.ctb + (c / w) * d * w + (c % w);
   for (int64_t t = threadIdx.x; t < dpad; t += blockDim.x) {
     const double val = t < d ? row[t] : 0.0;
     v.c32[c * dpad + t] = (float)val;
     if (t < d) {
       v.ct64[t * ld + c] = val;  // C^T: re-check, CSR
-      ct32s[t * w] = (float)val;
+      ctbs[t * w] = __builtin_bit_cast(uint16_t, (__bf16)(float)val);
     }
   }
   // sequential over t: sklearn row_norms(squared=True) order
