@@ -167,6 +167,37 @@ __global__ void __launch_bounds__(NB)
   }
 }
 
+// sklearn's squared CSR distance of query row [qa, qb) (|q|^2 = xx) to fit
+// row j, clamped at 0 (the arithmetic of the comment below).
+__device__ __forceinline__ double csr_pair_r(
+    int64_t qa, int64_t qb, const int32_t *__restrict__ qi,
+    const double *__restrict__ qd, double xx, const int64_t *__restrict__ xp,
+    const int32_t *__restrict__ xi, const double *__restrict__ xd, int64_t j,
+    int f32) {
+  const int64_t a = xp[j], b = xp[j + 1];
+  double yy = 0.0, dot = 0.0;
+  int64_t t = qa;
+  int32_t qc = t < qb ? qi[t] : INT32_MAX;
+  for (int64_t u = a; u < b; ++u) {
+    const int32_t c = xi[u];
+    const double v = xd[u];
+    yy += v * v;
+    while (qc < c) {
+      ++t;
+      qc = t < qb ? qi[t] : INT32_MAX;
+    }
+    if (qc == c) dot += qd[t] * v;
+  }
+  double r = -2.0 * dot;
+  r += xx;
+  r += yy;
+  if (f32) {  // float32 Subsets: the squares rounded to float32 first
+    const float r32 = (float)r;
+    return r32 < 0.f ? 0.0 : (double)r32;
+  }
+  return r < 0.0 ? 0.0 : r;
+}
+
 // Sparse kNN partial lists.  sklearn picks brute force for CSR fit data and,
 // its ArgKmin reduction refusing sparse-sparse pairs, ranks by
 // pairwise_distances_chunked(squared=True): r = max(((-2 q.x) + ||q||^2) +
@@ -208,33 +239,11 @@ __global__ void __launch_bounds__(NB)
   const int64_t j0 = (int64_t)p * plen;
   const int64_t j1 = std::min<int64_t>(nx, j0 + plen);
   for (int64_t j = j0; j < j1; ++j) {
-    const int64_t a = xp[j], b = xp[j + 1];
-    double yy = 0.0, dot = 0.0;
-    int64_t t = qa;
-    int32_t qc = t < qb ? qi[t] : INT32_MAX;
-    for (int64_t u = a; u < b; ++u) {
-      const int32_t c = xi[u];
-      const double v = xd[u];
-      yy += v * v;
-      while (qc < c) {
-        ++t;
-        qc = t < qb ? qi[t] : INT32_MAX;
-      }
-      if (qc == c) dot += qd[t] * v;
-    }
-    double r = -2.0 * dot;
-    r += xx;
-    r += yy;
-    if (f32) {  // float32 Subsets: the squares rounded to float32 first
-      const float r32 = (float)r;
-      r = r32 < 0.f ? 0.0 : (double)r32;
-    } else {
-      r = r < 0.0 ? 0.0 : r;
-    }
     // (finite data whose squares overflow: inf - inf = NaN, ranked after
     // +inf).  A later pass: only (r, j) strictly after the previous pass's
     // last.
-    const uint64_t rk = rkey(r);
+    const uint64_t rk = rkey(csr_pair_r(qa, qb, qi, qd, xx, xp, xi, xd, j,
+                                        f32));
     if (rk > fr || (rk == fr && (int)j > fi)) top.push(rk, (int)j);
   }
   if (!live) return;
@@ -279,6 +288,187 @@ __global__ void __launch_bounds__(NB)
         fli[q] = top.i[s];
       }
     }
+}
+
+// ---------------------------------------------------------------------------
+// kNN beyond 32 neighbours in two scans (32 < kn <= KB_KN_MAX).
+//   scan 1  k_knn_part / k_knn_csr_part with K = 32 over Pb >= kn/32 + 1
+//           partitions: per query, Pb sorted lists of 32.
+//   k_knn_thresh  block per query: the kn-th smallest (key, index) of the
+//           union of those lists.  The union is a subset of the fit rows, so
+//           this is an upper bound (tk, ti) of the true kn-th pair.
+//   scan 2  k_knn_cand / k_knn_csr_cand: the same pair arithmetic; every
+//           (key, j) <= (tk, ti) is appended to the query's candidate list
+//           (per-lane atomics on the lane's own counter: about kn appends per
+//           query over the whole scan).
+//   k_knn_final  block per query: bitonic sort of the candidates in LDS by
+//           (key, index), the first kn written out.  A list longer than
+//           KB_CAP raises a flag and the host reruns the call in passes of 32.
+// Two scans of nq x nx pairs instead of ceil(kn / 32) (kn = 1000: 32).
+// ---------------------------------------------------------------------------
+constexpr int KB_CAP = 4096;      // candidates per query (LDS sort)
+constexpr int KB_KN_MAX = 2048;   // kn this path takes
+constexpr int KB_P_MAX = KB_CAP / 32;
+constexpr int64_t KB_QC = 8192;   // queries per chunk (workspace bound)
+
+__device__ __forceinline__ bool key_le(uint64_t a, int ia, uint64_t b,
+                                       int ib) {
+  return a < b || (a == b && ia <= ib);
+}
+
+// Bitonic sort of n <= KB_CAP (key, index) pairs in LDS, ascending.
+__device__ void lds_sort_keys(uint64_t *sk, int *si, int n) {
+  int p2 = 2;
+  while (p2 < n) p2 <<= 1;
+  for (int e = n + threadIdx.x; e < p2; e += NB) {
+    sk[e] = KEY_EMPTY;
+    si[e] = INT32_MAX;
+  }
+  __syncthreads();
+  for (int size = 2; size <= p2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int e = threadIdx.x; e < p2; e += NB) {
+        const int f = e ^ stride;
+        if (f > e) {
+          const bool up = (e & size) == 0;
+          const bool gt = !key_le(sk[e], si[e], sk[f], si[f]);
+          if (gt == up) {
+            const uint64_t tk = sk[e];
+            sk[e] = sk[f];
+            sk[f] = tk;
+            const int ti = si[e];
+            si[e] = si[f];
+            si[f] = ti;
+          }
+        }
+      }
+      __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(NB)
+    k_knn_thresh(const double *__restrict__ pr, const int *__restrict__ pi,
+                 int64_t nq, int P, int kn, uint64_t *__restrict__ thk,
+                 int *__restrict__ thi, unsigned *__restrict__ cc) {
+  __shared__ uint64_t sk[KB_CAP];
+  __shared__ int si[KB_CAP];
+  const int64_t q = blockIdx.x;
+  if (q >= nq) return;
+  const int m = P * 32;
+  for (int e = threadIdx.x; e < m; e += NB) {
+    sk[e] = (uint64_t)__double_as_longlong(pr[q * m + e]);
+    si[e] = pi[q * m + e];
+  }
+  lds_sort_keys(sk, si, m);
+  if (threadIdx.x == 0) {
+    thk[q] = sk[kn - 1];
+    thi[q] = si[kn - 1];
+    cc[q] = 0;
+  }
+}
+
+template <int MAXD>
+__global__ void __launch_bounds__(NB)
+    k_knn_cand(const double *__restrict__ Q, int64_t nq, int64_t ldq,
+               const double *__restrict__ X, int64_t nx, int64_t ldx, int d,
+               int64_t plen, const uint64_t *__restrict__ thk,
+               const int *__restrict__ thi, unsigned *__restrict__ cc,
+               uint64_t *__restrict__ ck, int *__restrict__ ci) {
+  const int lane = threadIdx.x & 63;
+  const int64_t qg = (int64_t)blockIdx.x * (NB / 64) +
+                     __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t q = qg * 64 + lane;
+  if (qg * 64 >= nq) return;  // wave-uniform
+  const bool live = q < nq;
+  const double *qrow = Q + (live ? q : 0) * ldq;
+  double qv[MAXD > 0 ? MAXD : 1];
+  if constexpr (MAXD > 0) {
+#pragma unroll
+    for (int t = 0; t < MAXD; ++t) qv[t] = t < d ? qrow[t] : 0.0;
+  }
+  const uint64_t tk = live ? thk[q] : 0;
+  const int ti = live ? thi[q] : -1;
+  const int64_t j0 = (int64_t)blockIdx.y * plen;
+  const int64_t j1 = std::min<int64_t>(nx, j0 + plen);
+  cdouble *xc = (cdouble *)X;
+  for (int64_t j = j0; j < j1; ++j) {
+    const uint64_t r = rkey(seq_r<MAXD>(qv, qrow, xc + j * ldx, d));
+    if (live && key_le(r, (int)j, tk, ti)) {
+      const unsigned pos = atomicAdd(cc + q, 1u);
+      if (pos < (unsigned)KB_CAP) {
+        ck[q * KB_CAP + pos] = r;
+        ci[q * KB_CAP + pos] = (int)j;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NB)
+    k_knn_csr_cand(const int64_t *__restrict__ qp,
+                   const int32_t *__restrict__ qi,
+                   const double *__restrict__ qd, int64_t nq,
+                   const int64_t *__restrict__ xp,
+                   const int32_t *__restrict__ xi,
+                   const double *__restrict__ xd, int64_t nx, int64_t plen,
+                   int f32, const uint64_t *__restrict__ thk,
+                   const int *__restrict__ thi, unsigned *__restrict__ cc,
+                   uint64_t *__restrict__ ck, int *__restrict__ ci) {
+  const int lane = threadIdx.x & 63;
+  const int64_t qg = (int64_t)blockIdx.x * (NB / 64) +
+                     __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t q = qg * 64 + lane;
+  if (qg * 64 >= nq) return;  // wave-uniform
+  const bool live = q < nq;
+  const int64_t qa = live ? qp[q] : 0;
+  const int64_t qb = live ? qp[q + 1] : 0;
+  double xx = 0.0;
+  for (int64_t t = qa; t < qb; ++t) {
+    const double v = qd[t];
+    xx += v * v;
+  }
+  const uint64_t tk = live ? thk[q] : 0;
+  const int ti = live ? thi[q] : -1;
+  const int64_t j0 = (int64_t)blockIdx.y * plen;
+  const int64_t j1 = std::min<int64_t>(nx, j0 + plen);
+  for (int64_t j = j0; j < j1; ++j) {
+    const uint64_t r =
+        rkey(csr_pair_r(qa, qb, qi, qd, xx, xp, xi, xd, j, f32));
+    if (live && key_le(r, (int)j, tk, ti)) {
+      const unsigned pos = atomicAdd(cc + q, 1u);
+      if (pos < (unsigned)KB_CAP) {
+        ck[q * KB_CAP + pos] = r;
+        ci[q * KB_CAP + pos] = (int)j;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NB)
+    k_knn_final(const unsigned *__restrict__ cc,
+                const uint64_t *__restrict__ ck, const int *__restrict__ ci,
+                int64_t nq, int kn, double *__restrict__ out_d,
+                int64_t *__restrict__ out_i, int64_t ldo, int f32,
+                unsigned *__restrict__ overflow) {
+  __shared__ uint64_t sk[KB_CAP];
+  __shared__ int si[KB_CAP];
+  const int64_t q = blockIdx.x;
+  if (q >= nq) return;
+  const unsigned c = cc[q];
+  if (c > (unsigned)KB_CAP) {  // block-uniform
+    if (threadIdx.x == 0) atomicOr(overflow, 1u);
+    return;
+  }
+  const int m = (int)c;  // >= kn: the threshold pair and all before it
+  for (int e = threadIdx.x; e < m; e += NB) {
+    sk[e] = ck[q * KB_CAP + e];
+    si[e] = ci[q * KB_CAP + e];
+  }
+  lds_sort_keys(sk, si, m);
+  for (int e = threadIdx.x; e < kn; e += NB) {
+    const double r = key_r(sk[e]);
+    out_d[q * ldo + e] = f32 ? (double)(float)sqrt(r) : sqrt(r);
+    out_i[q * ldo + e] = (int64_t)si[e];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -693,6 +883,105 @@ int radius_csr_args(const int64_t *indptr, const int32_t *indices,
   return 0;
 }
 
+// The two-scan path (kn in (32, KB_KN_MAX]): partitions and workspace.
+// Pb >= kn / 32 + 1 partitions such that the union of their top-32 lists
+// holds >= kn rows (every row when partitions are shorter than 32).
+bool kb_applies(int64_t kn) { return kn > 32 && kn <= KB_KN_MAX; }
+
+void kb_grid(int64_t nq, int64_t nx, int64_t kn, int64_t *plen, int *P) {
+  int64_t pl0;
+  int P0;
+  knn_grid(nq, nx, &pl0, &P0);
+  for (int64_t want = std::max<int64_t>(P0, kn / 32 + 1);; ++want) {
+    const int64_t w = std::min<int64_t>({want, (int64_t)KB_P_MAX, nx});
+    const int64_t pl = (nx + w - 1) / w;
+    const int64_t np = (nx + pl - 1) / pl;
+    int64_t uni = 0;
+    for (int64_t p = 0; p < np; ++p)
+      uni += std::min<int64_t>(32, std::min(nx, (p + 1) * pl) - p * pl);
+    if (uni >= kn || w >= KB_P_MAX || w >= nx) {
+      *plen = pl;
+      *P = (int)np;
+      return;
+    }
+  }
+}
+
+struct KbWs {
+  double *pr;
+  int *pi;
+  uint64_t *thk;
+  int *thi;
+  unsigned *cc;
+  uint64_t *ck;
+  int *ci;
+  unsigned *flag;
+};
+
+size_t kb_layout(int64_t qc, int P, char *base, KbWs *w) {
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o += (bytes + 255) & ~(size_t)255;
+    return base ? base + at : nullptr;
+  };
+  const size_t m = (size_t)qc * P * 32;
+  char *a = take(m * 8), *b = take(m * 4), *c = take((size_t)qc * 8),
+       *d = take((size_t)qc * 4), *e = take((size_t)qc * 4),
+       *f = take((size_t)qc * KB_CAP * 8), *g = take((size_t)qc * KB_CAP * 4),
+       *h = take(4);
+  if (w) *w = KbWs{(double *)a, (int *)b, (uint64_t *)c, (int *)d,
+                   (unsigned *)e, (uint64_t *)f, (int *)g, (unsigned *)h};
+  return o;
+}
+
+size_t kb_bytes(int64_t nq, int64_t nx, int64_t kn) {
+  int64_t plen;
+  int P;
+  kb_grid(nq, nx, kn, &plen, &P);
+  return kb_layout(std::min<int64_t>(std::max<int64_t>(nq, 1), KB_QC), P,
+                   nullptr, nullptr);
+}
+
+// One chunk-looped two-scan call.  scan(q0, qc, g, plen, P, pr, pi) and
+// cand(q0, qc, g, plen, thk, thi, cc, ck, ci) launch the dense or CSR
+// kernels; *overflow = 1 when a candidate list outgrew KB_CAP (the caller
+// reruns in passes).
+template <class Scan, class Cand>
+int kb_run(int64_t nq, int64_t nx, int64_t kn, void *ws, int f32,
+           double *out_dist, int64_t *out_idx, hipStream_t s, Scan scan,
+           Cand cand, bool *overflow) {
+  int64_t plen;
+  int P;
+  kb_grid(nq, nx, kn, &plen, &P);
+  KbWs w;
+  kb_layout(std::min<int64_t>(nq, KB_QC), P, (char *)ws, &w);
+  if (hipMemsetAsync(w.flag, 0, 4, s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "knn: memset");
+  for (int64_t q0 = 0; q0 < nq; q0 += KB_QC) {
+    const int64_t qc = std::min<int64_t>(KB_QC, nq - q0);
+    const dim3 g((unsigned)((qc + 255) / 256), (unsigned)P);
+    if (int r = scan(q0, qc, g, plen, P, w.pr, w.pi)) return r;
+    k_knn_thresh<<<(unsigned)qc, NB, 0, s>>>(w.pr, w.pi, qc, P, (int)kn,
+                                             w.thk, w.thi, w.cc);
+    if (int r = check_launch("knn threshold")) return r;
+    if (int r = cand(q0, qc, g, plen, w.thk, w.thi, w.cc, w.ck, w.ci))
+      return r;
+    k_knn_final<<<(unsigned)qc, NB, 0, s>>>(w.cc, w.ck, w.ci, qc, (int)kn,
+                                            out_dist + q0 * kn,
+                                            out_idx + q0 * kn, kn, f32,
+                                            w.flag);
+    if (int r = check_launch("knn final sort")) return r;
+  }
+  unsigned fl = 0;
+  if (hipMemcpyAsync(&fl, w.flag, 4, hipMemcpyDeviceToHost, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "knn: reading the overflow flag");
+  *overflow = fl != 0;
+  return 0;
+}
+
 }  // namespace
 }  // namespace dkm
 
@@ -707,8 +996,10 @@ size_t dkm_knn_workspace_bytes(int64_t nq, int64_t nx, int64_t kn) {
   knn_grid(std::max<int64_t>(nq, 1), nx, &plen, &P);
   const int K = knn_k(std::min<int64_t>(kn, 32));
   const int64_t q = std::max<int64_t>(nq, 1);
-  // partial lists of one pass, then the per-query floor (r, index)
-  return (size_t)q * P * K * (8 + 4) + (size_t)q * (8 + 4) + 512;
+  // partial lists of one pass, then the per-query floor (r, index); the
+  // two-scan path's chunk when it applies (its fallback is the passes)
+  const size_t passes = (size_t)q * P * K * (8 + 4) + (size_t)q * (8 + 4) + 512;
+  return kb_applies(kn) ? std::max(passes, kb_bytes(nq, nx, kn)) : passes;
 }
 
 int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
@@ -723,6 +1014,32 @@ int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
     return fail(DKM_E_WORKSPACE, "knn: workspace smaller than "
                                  "dkm_knn_workspace_bytes()");
   hipStream_t s = (hipStream_t)stream;
+  const int maxd = maxd_of(d);
+  if (kb_applies(kn)) {
+    bool over = false;
+    auto scan = [&](int64_t q0, int64_t qc, dim3 g, int64_t pl, int P,
+                    double *pr, int *pi) {
+      return knn_dispatch<32>(maxd, g, s, Q + q0 * ldq, qc, ldq, X, nx, ldx,
+                              (int)d, pl, P, pr, pi, nullptr, nullptr);
+    };
+    auto cand = [&](int64_t q0, int64_t qc, dim3 g, int64_t pl,
+                    const uint64_t *thk, const int *thi, unsigned *cc,
+                    uint64_t *ck, int *ci) {
+      const double *Qc = Q + q0 * ldq;
+      switch (maxd) {
+        case 8: k_knn_cand<8><<<g, NB, 0, s>>>(Qc, qc, ldq, X, nx, ldx, (int)d, pl, thk, thi, cc, ck, ci); break;
+        case 16: k_knn_cand<16><<<g, NB, 0, s>>>(Qc, qc, ldq, X, nx, ldx, (int)d, pl, thk, thi, cc, ck, ci); break;
+        case 32: k_knn_cand<32><<<g, NB, 0, s>>>(Qc, qc, ldq, X, nx, ldx, (int)d, pl, thk, thi, cc, ck, ci); break;
+        case 64: k_knn_cand<64><<<g, NB, 0, s>>>(Qc, qc, ldq, X, nx, ldx, (int)d, pl, thk, thi, cc, ck, ci); break;
+        default: k_knn_cand<0><<<g, NB, 0, s>>>(Qc, qc, ldq, X, nx, ldx, (int)d, pl, thk, thi, cc, ck, ci); break;
+      }
+      return check_launch("knn candidates");
+    };
+    if (int r = kb_run(nq, nx, kn, ws, 0, out_dist, out_idx, s, scan, cand,
+                       &over))
+      return r;
+    if (!over) return 0;
+  }
   int64_t plen;
   int P;
   knn_grid(nq, nx, &plen, &P);
@@ -733,7 +1050,6 @@ int dkm_knn_f64(const double *Q, int64_t nq, int64_t ldq, const double *X,
                            ~(uintptr_t)255);
   int *fli = (int *)(flr + nq);
   const dim3 g((unsigned)((nq + 255) / 256), (unsigned)P);
-  const int maxd = maxd_of(d);
   for (int64_t c0 = 0; c0 < kn; c0 += 32) {
     const int kk = (int)std::min<int64_t>(32, kn - c0);
     const int K = knn_k(kk);
@@ -776,6 +1092,28 @@ int dkm_knn_csr_f64(const int64_t *q_indptr, const int32_t *q_indices,
     return fail(DKM_E_WORKSPACE, "knn csr: workspace smaller than "
                                  "dkm_knn_workspace_bytes()");
   hipStream_t s = (hipStream_t)stream;
+  const int f32 = out_f32 ? 1 : 0;
+  if (kb_applies(kn)) {
+    bool over = false;
+    auto scan = [&](int64_t q0, int64_t qc, dim3 g, int64_t pl, int P,
+                    double *pr, int *pi) {
+      return knn_csr_launch<32>(g, s, q_indptr + q0, q_indices, q_data, qc,
+                                x_indptr, x_indices, x_data, nx, pl, P, f32,
+                                pr, pi, nullptr, nullptr);
+    };
+    auto cand = [&](int64_t q0, int64_t qc, dim3 g, int64_t pl,
+                    const uint64_t *thk, const int *thi, unsigned *cc,
+                    uint64_t *ck, int *ci) {
+      k_knn_csr_cand<<<g, NB, 0, s>>>(q_indptr + q0, q_indices, q_data, qc,
+                                      x_indptr, x_indices, x_data, nx, pl,
+                                      f32, thk, thi, cc, ck, ci);
+      return check_launch("knn csr candidates");
+    };
+    if (int r = kb_run(nq, nx, kn, ws, f32, out_dist, out_idx, s, scan, cand,
+                       &over))
+      return r;
+    if (!over) return 0;
+  }
   int64_t plen;
   int P;
   knn_grid(nq, nx, &plen, &P);

@@ -186,15 +186,6 @@ __global__ void __launch_bounds__(CSR_BLOCK)
 #pragma unroll
         for (int h = 0; h < CSR_W; ++h) dot[p][h] = 0.f;
       const bool first = jp == j_lo;
-      // the pass's |c_j|^2 load early (used after the gathers)
-      float cnv[NP][CSR_W];
-#pragma unroll
-      for (int p = 0; p < NP; ++p)
-#pragma unroll
-        for (int h = 0; h < CSR_W; ++h) {
-          const int j = jp + CSR_PASS * p + CSR_W * gl + h;
-          cnv[p][h] = j < j_hi ? cn[j] : 0.f;
-        }
       for (int64_t c0 = a; c0 < b; c0 += CSR_G) {
         const int cnt = (int)min<int64_t>(CSR_G, b - c0);
         const int64_t u = (c0 - a) / CSR_G;
@@ -267,7 +258,9 @@ __global__ void __launch_bounds__(CSR_BLOCK)
         for (int h = 0; h < CSR_W; ++h) {
           const int j = jp + CSR_PASS * p + CSR_W * gl + h;
           if (j < j_hi) {  // centres ascending per lane: strict < = first
-            const float sj = fmaf(-2.f, dot[p][h], cnv[p][h]);
+            // |c_j|^2 loaded here, not before the walk: 32 VGPRs held over
+            // the gathers cost a wave per SIMD
+            const float sj = fmaf(-2.f, dot[p][h], cn[j]);
             if (sj < s1) {
               s2 = s1;
               s1 = sj;

@@ -64,15 +64,30 @@ def test_kneighbors_reference_golden(name):
     (500, 3000, 5, 33, 5),       # n_neighbors > 32: a second pass of one
     (300, 2000, 12, 100, 6),     # four passes, the last of 4 columns
     (200, 700, 70, 64, 7),       # exactly two full passes, d > 64
+    (300, 20000, 5, 1000, 8),    # the two-scan path (32 < kn <= 2048)
+    (130, 6144, 70, 2048, 9),    # its largest kn, d > 64
+    (64, 1200, 3, 1200, 10),     # kn = nx: every row
 ])
 def test_kneighbors_vs_oracle(nq, nx, d, kn, seed):
     rng = np.random.default_rng(seed)
     xf = rng.standard_normal((nx, d)) * rng.uniform(0.5, 3.0, d)
     xq = rng.standard_normal((nq, d)) * rng.uniform(0.5, 3.0, d)
-    dist, ind = _knn(xf, xq, 1000, kn, 250)
+    # (the reference fits sklearn per Subset: n_neighbors <= subset rows)
+    dist, ind = _knn(xf, xq, max(1000, kn), kn, 250)
     od, oi = orc.kneighbors_exact(xf, xq, kn)
     assert np.array_equal(ind, oi)
     assert np.array_equal(dist, od)
+
+
+def test_kneighbors_two_scan_overflow_falls_back():
+    """Fit rows in distance order: the union of the partitions' top-32 lists
+    gives a loose threshold, the candidate lists outgrow their cap and the
+    call reruns in passes of 32 -- same result."""
+    xf = np.arange(60000, dtype=np.float64)[:, None] * np.ones((1, 2))
+    xq = np.array([[0.25, 0.0], [3.0, 3.0], [59999.0, 1.0]])
+    dist, ind = _knn(xf, xq, 60000, 1000, 3)
+    od, oi = orc.kneighbors_exact(xf, xq, 1000)
+    assert np.array_equal(ind, oi) and np.array_equal(dist, od)
 
 
 def test_kneighbors_ties_by_index():
@@ -309,6 +324,7 @@ def test_sparse_kneighbors_reference_golden(name):
     (700, 2000, 100000, 0.00001, 6, "uniform"),  # ~37% empty rows: ties
     (129, 300, 30, 0.2, 1, "uniform"),         # ragged wave, one neighbour
     (300, 1500, 20, 0.3, 70, "big"),           # 1e200 entries: inf rows
+    (200, 12000, 40, 0.1, 1000, "grid"),       # two-scan path, many ties
     (256, 600, 40, 0.2, 9, "unsorted"),        # unsorted rows read sorted
 ])
 def test_sparse_kneighbors_vs_oracle(nq, nx, d, dens, kn, kind):
