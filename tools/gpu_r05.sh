@@ -7,6 +7,7 @@
 #   c3it      C3 bench line under a rocprofv3 kernel trace, per iteration
 #   c4it      C4 bench line under a rocprofv3 kernel trace, per iteration
 #   c3ab      C3 bench line, main vs libdkm_old.so, two rounds
+#   c2ab      C2 headline line, main vs libdkm_$AB.so (AB env, default w32pf2), two rounds
 #   bench     default bench.py
 TAG=${1:-r05}; shift
 OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
@@ -36,6 +37,12 @@ for s in "$@"; do
       [ -n "$DB" ] && python tools/prof_iters.py $DB > $P/iters.txt 2>&1 && rm -f $DB
       find $P -type f ! -name 'iters.txt' ! -name '*kernel_stats.csv' -delete
       cut -c1-300 $P/iters.txt ;;
+    c2it) P=$OUT/${TAG}_c2it; mkdir -p $P
+      step c2it 300 rocprofv3 --kernel-trace --stats -d $P -o run -- python bench.py --steps 8 --warmup 2 --no-cpu --only-headline
+      DB=$(find $P -name '*.db' | head -1)
+      [ -n "$DB" ] && python tools/prof_iters.py $DB > $P/iters.txt 2>&1 && rm -f $DB
+      find $P -type f ! -name 'iters.txt' -delete
+      cut -c1-300 $P/iters.txt ;;
     c4it) P=$OUT/${TAG}_c4it; mkdir -p $P
       step c4it 400 rocprofv3 --kernel-trace --stats -d $P -o run -- $C4
       DB=$(find $P -name "*.db" | head -1); [ -n "$DB" ] && python tools/prof_iters.py $DB > $P/iters.txt 2>&1 && rm -f $DB; find $P -type f ! -name iters.txt -delete
@@ -44,6 +51,11 @@ for s in "$@"; do
         if [ $v = old ]; then export DKM_LIB=$OLD; else unset DKM_LIB; fi
         step c3_$v$r 300 $C3
         python -c "import json;d=json.loads([l for l in open('$OUT/${TAG}_c3_$v$r.log') if l.startswith('{')][-1]);print('$v', round(d['ms_per_step'],3), 'fit', round(d['fit_ms_per_iter'],2), 'kern', round(d['roofline']['kernel_ms'],3))"
+      done; done; unset DKM_LIB ;;
+    c2ab) V=${AB:-w32pf2}; for r in 1 2; do for v in main $V; do
+        if [ $v = main ]; then unset DKM_LIB; else export DKM_LIB=$PWD/dislib_amd/libdkm_$v.so; fi
+        step c2_$v$r 300 python bench.py --steps 20 --warmup 3 --no-cpu --only-headline
+        python -c "import json;d=json.loads([l for l in open('$OUT/${TAG}_c2_$v$r.log') if l.startswith('{')][-1]);print('$v', round(d['ms_per_step'],3), 'fit', round(d['fit_ms_per_iter'],2), 'kern', round(d['roofline']['kernel_ms'],3))"
       done; done; unset DKM_LIB ;;
     bench) step bench 900 python bench.py ;;
     *) echo "unknown step $s"; exit 2 ;;
