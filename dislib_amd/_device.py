@@ -222,10 +222,28 @@ class Workspace:
         if self.nbytes == 0:
             raise _lib.DkmError("dkm_workspace_bytes: bad k/d")
         self.buf = t.zeros(self.nbytes, dtype=t.uint8, device=device)
+        preload(self.buf.device)
 
     @property
     def p(self):
         return ctypes.c_void_p(self.buf.data_ptr())
+
+
+_PRELOADED = set()
+
+
+def preload(device):
+    """Load the library's kernels on ``device`` now (``dkm_preload``), once
+    per process and device: the runtime loads each source file's kernels on
+    first launch, several ms apiece, which otherwise lands inside the first
+    Lloyd iterations."""
+    t = torch()
+    idx = t.device(device).index
+    if idx in _PRELOADED:
+        return
+    with on(device):
+        _lib.check(_lib.lib().dkm_preload(), "dkm_preload")
+    _PRELOADED.add(idx)
 
 
 # ---------------------------------------------------------------------------

@@ -29,6 +29,7 @@ _u64 = ctypes.c_uint64
 # name -> (restype, argtypes): every entry point of include/dkm.h
 SIGNATURES = {
     "dkm_abi_version": (_i32, []),
+    "dkm_preload": (_i32, []),
     "dkm_last_error": (ctypes.c_char_p, []),
     "dkm_workspace_bytes": (_sz, [_i64, _i64, _i64]),
     "dkm_prepare_centers": (_i32, [_p, _i64, _i64, _i32, _p, _sz, _p, _p]),

@@ -1516,3 +1516,14 @@ template int launch_screen_b2<float>(const float *, int64_t, int, int64_t, int,
                                      int, hipStream_t, int *, XImage);
 
 }  // namespace dkm
+
+// Code-object preload (dkm_preload): the runtime loads this file's kernels
+// on first use of any of them; an attribute query here does it up front.
+namespace dkm {
+__global__ void k_tu_b2() {}
+int preload_b2() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, (const void *)k_tu_b2) == hipSuccess ? 0
+                                                                       : 1;
+}
+}  // namespace dkm

@@ -114,3 +114,14 @@ template int launch_cand2_leaf<float>(const float *, int, int64_t,
                                       hipStream_t);
 
 }  // namespace dkm
+
+// Code-object preload (dkm_preload): the runtime loads this file's kernels
+// on first use of any of them; an attribute query here does it up front.
+namespace dkm {
+__global__ void k_tu_cand() {}
+int preload_cand() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, (const void *)k_tu_cand) == hipSuccess ? 0
+                                                                       : 1;
+}
+}  // namespace dkm

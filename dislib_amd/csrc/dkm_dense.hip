@@ -3283,3 +3283,14 @@ int dkm_build_flags(void) {
 }
 
 }  // extern "C"
+
+// Code-object preload (dkm_preload): the runtime loads this file's kernels
+// on first use of any of them; an attribute query here does it up front.
+namespace dkm {
+__global__ void k_tu_dense() {}
+int preload_dense() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, (const void *)k_tu_dense) == hipSuccess ? 0
+                                                                       : 1;
+}
+}  // namespace dkm

@@ -1237,3 +1237,14 @@ template int gemm_image<float>(const float *, int64_t, int, int64_t,
                                const XImage &, hipStream_t);
 
 }  // namespace dkm
+
+// Code-object preload (dkm_preload): the runtime loads this file's kernels
+// on first use of any of them; an attribute query here does it up front.
+namespace dkm {
+__global__ void k_tu_gemm() {}
+int preload_gemm() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, (const void *)k_tu_gemm) == hipSuccess ? 0
+                                                                       : 1;
+}
+}  // namespace dkm

@@ -20,6 +20,15 @@ constexpr int WAVE = 64;
 // ---------------------------------------------------------------------------
 void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
+// Per-file code-object preload (each .hip file's kernels load on first use).
+int preload_dense();
+int preload_b2();
+int preload_sorted();
+int preload_cand();
+int preload_sparse();
+int preload_gemm();
+int preload_sums();
+int preload_neighbors();
 int check_launch(const char *what);
 
 // ---------------------------------------------------------------------------

@@ -611,3 +611,14 @@ int launch_screen_sorted(int64_t n, int d, int k, const WsView &v,
 }
 
 }  // namespace dkm
+
+// Code-object preload (dkm_preload): the runtime loads this file's kernels
+// on first use of any of them; an attribute query here does it up front.
+namespace dkm {
+__global__ void k_tu_sorted() {}
+int preload_sorted() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, (const void *)k_tu_sorted) == hipSuccess ? 0
+                                                                       : 1;
+}
+}  // namespace dkm

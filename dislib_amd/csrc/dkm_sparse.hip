@@ -627,3 +627,14 @@ int dkm_predict_csr_f64(const int64_t *indptr, const int32_t *indices,
 }
 
 }  // extern "C"
+
+// Code-object preload (dkm_preload): the runtime loads this file's kernels
+// on first use of any of them; an attribute query here does it up front.
+namespace dkm {
+__global__ void k_tu_sparse() {}
+int preload_sparse() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, (const void *)k_tu_sparse) == hipSuccess ? 0
+                                                                       : 1;
+}
+}  // namespace dkm

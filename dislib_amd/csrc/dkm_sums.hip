@@ -425,3 +425,14 @@ template int sorted_sums<double>(const double *, int64_t, int64_t, int,
                                  int, double *, const WsView &, hipStream_t);
 
 }  // namespace dkm
+
+// Code-object preload (dkm_preload): the runtime loads this file's kernels
+// on first use of any of them; an attribute query here does it up front.
+namespace dkm {
+__global__ void k_tu_sums() {}
+int preload_sums() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, (const void *)k_tu_sums) == hipSuccess ? 0
+                                                                       : 1;
+}
+}  // namespace dkm

@@ -481,6 +481,15 @@ int dkm_abi_version(void) { return DKM_ABI_VERSION; }
 
 const char *dkm_last_error(void) { return g_err.c_str(); }
 
+int dkm_preload(void) {
+  hipFuncAttributes a;
+  int bad = hipFuncGetAttributes(&a, (const void *)k_prepare) != hipSuccess;
+  bad += preload_dense() + preload_b2() + preload_sorted() + preload_cand() +
+         preload_sparse() + preload_gemm() + preload_sums() +
+         preload_neighbors();
+  return bad ? fail(DKM_E_LAUNCH, "preload: kernel attribute query") : 0;
+}
+
 size_t dkm_workspace_bytes(int64_t k, int64_t d, int64_t n_queue) {
   if (k <= 0 || d <= 0) return 0;
   return ws_bytes(k, d, n_queue);

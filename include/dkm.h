@@ -69,6 +69,13 @@ extern "C" {
 #define DKM_SUMS_RECIP 2 /* sparse: centre = sum * (1.0/count) (scipy divide) */
 
 int dkm_abi_version(void);
+
+/* Load every kernel's code object now instead of at its first launch (the
+ * runtime loads a source file's kernels lazily, several ms per file: the
+ * first Lloyd iterations paid it inside the fit).  Optional; idempotent.
+ * Replaces nothing in the reference (PyCOMPSs workers import their
+ * libraries before the first task). */
+int dkm_preload(void);
 const char *dkm_last_error(void);
 
 /* Workspace needed for k centres of d features and up to n_queue re-check

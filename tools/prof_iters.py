@@ -15,6 +15,8 @@ def main(path):
     it, t0 = -1, {}
     per = collections.defaultdict(collections.Counter)
     last_end = None
+    last_short = None
+    gaps = collections.defaultdict(list)
     for name, s, e in rows:
         m = re.search(r"\b(k_\w+|__amd\w+|\w+_kernel)", name)
         short = m.group(1) if m else name[:20]
@@ -24,17 +26,26 @@ def main(path):
             if last_end is not None and it > 0:
                 # GPU idle between the iterations (host sync + launches)
                 per[it - 1]["GAP_NEXT"] = (s - crit_end) / 1e6
+        if last_end is not None and short != "k_prepare" and it >= 0:
+            gaps[it].append(((s - last_end) / 1e6, last_short, short))
         per[it][short] += (e - s) / 1e6
         per[it]["BUSY"] += (e - s) / 1e6
         if short == "k_criterion":
             per[it]["WALL"] = (e - t0[it]) / 1e6
             crit_end = e
         last_end = e
+        last_short = short
     for i in sorted(per):
         if i < 0:
             continue
         items = sorted(per[i].items(), key=lambda x: -x[1])
         print(i, " ".join("%s=%.2f" % kv for kv in items if kv[1] > 0.05))
+    # the largest idle gaps inside each iteration (host work between launches)
+    for i in sorted(gaps):
+        big = sorted(gaps[i], reverse=True)[:3]
+        big = [g for g in big if g[0] > 0.3]
+        if big:
+            print("  gaps", i, " ".join("%.2f(%s->%s)" % g for g in big))
 
 
 if __name__ == "__main__":
