@@ -1288,6 +1288,34 @@ __global__ void k_perm_sorted(const int32_t *__restrict__ sitems,
   }
 }
 
+// The image's initial label copy straight from the sort's cluster offsets:
+// row i of the label-sorted image carries cluster c for soff[c] <= i <
+// soff[c + 1], and -1 past soff[k] (unlabelled rows, padding) -- what k_plab's
+// full pass (plab[i] = lab[perm[i]], a random 4-B gather per row: 3 ms at
+// C3) computes, from a binary search per 4 rows and coalesced stores.
+__global__ void k_plab_offsets(const int32_t *__restrict__ soff, int k,
+                               int64_t ntot, int32_t *__restrict__ plab) {
+  const int64_t m = soff[k];
+  for (int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4;
+       i < ntot; i += (int64_t)gridDim.x * blockDim.x * 4) {
+    int lo = 0, hi = k;  // soff[lo] <= i < soff[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (soff[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    int32_t o[4];
+    int c = lo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t r = i + e;
+      while (c < k && soff[c + 1] <= r) ++c;  // empty clusters
+      o[e] = r < m ? c : -1;
+    }
+    *(int4 *)(plab + i) = make_int4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 __global__ void k_perm_unlabelled(const int32_t *__restrict__ lab, int64_t n,
                                   int k, const int32_t *__restrict__ nsorted,
                                   unsigned long long *count,
@@ -1391,8 +1419,8 @@ int launch_x_image_sorted(const TX *X, int64_t n, int d, int64_t ldx,
   const unsigned g = flat_grid(ntot, cus);
   k_perm_sorted<<<g, 256, 0, s>>>(v.sitems, v.soff + k, n, ntot, perm);
   k_perm_unlabelled<<<g, 256, 0, s>>>(labels, n, k, v.soff + k, cnt, perm);
-  k_plab<<<flat_grid((ntot + 3) / 4, cus), 256, 0, s>>>(
-      perm, labels, ntot, k, im.plab, 0, nullptr, nullptr, nullptr);
+  k_plab_offsets<<<flat_grid((ntot + 3) / 4, cus), 256, 0, s>>>(
+      v.soff, k, ntot, im.plab);
   if (int r = check_launch("sorted image: permutation")) return r;
   if (!acc) return launch_image_tiles<TX>(X, n, d, ldx, perm, im, cus, s);
   const int64_t nt = (n + 31) / 32;
