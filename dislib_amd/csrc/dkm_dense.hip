@@ -358,9 +358,18 @@ namespace dkm {
 #ifndef DKM_WPE
 #define DKM_WPE 6
 #endif
-#define DKM_SCREEN_WPE(NKS) \
+// CHUNK (fragments staged through LDS): one 512-thread block per CU (the
+// chunk fills the LDS), so 2 waves per SIMD whatever the registers: compiled
+// for 2 waves per EU (up to 256 VGPRs) instead of d <= 64's 4 -- C3
+// iteration 0's bf16x3 screen 60-61 -> 54 ms (r05nb kernel traces).  Two
+// 16-sample blocks per wave step (half the L2 -> LDS fragment traffic per
+// row) measured slower, 68.5 ms: NB_CHUNK stays 1.
+#ifndef DKM_NB_CHUNK
+#define DKM_NB_CHUNK 1
+#endif
+#define DKM_SCREEN_WPE(NKS, CHUNK) \
   __attribute__((amdgpu_waves_per_eu( \
-      DKM_WPE <= 0 ? 1 : (NKS) == 1 ? DKM_WPE : (NKS) == 2 ? 4 : 1)))
+      (CHUNK) ? 2 : DKM_WPE <= 0 ? 1 : (NKS) == 1 ? DKM_WPE : (NKS) == 2 ? 4 : 1)))
 constexpr int SB = DKM_SB;  // screen block: SB/64 waves share one LDS image
 
 // A/B switches, compile-time only (variants.sh -DDKM_AB_...=1; all off in the
@@ -558,7 +567,7 @@ __device__ __forceinline__ bool resolve_lane(
 // nothing) so that every wave reaches the chunk barriers.  L2 -> LDS traffic
 // per block step = all fragments (k * dpad * 4 B) per 16 * NB * SB/64 rows.
 template <int PREC, int NKS, int NB, bool VEC, class TX, bool CHUNK>
-__global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS)
+__global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
     k_screen(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
              WsView v, int32_t *__restrict__ lab_out, double *acc, int amode,
              int64_t base, int use_list, int chb) {
@@ -2386,7 +2395,7 @@ static int launch_screen_nks(const TX *X, int64_t end, int d, int64_t ldx,
                              int *nseg) {
 #define DKM_SCREEN_CASE(NKS, NB)                                             \
   case NKS:                                                                  \
-    return chb ? launch_screen_t<PREC, NKS, NB, VEC, TX, true>(              \
+    return chb ? launch_screen_t<PREC, NKS, DKM_NB_CHUNK, VEC, TX, true>(    \
                      X, end, d, ldx, k, v, lab_out, acc, amode, base, lds,   \
                      use_list, chb, s, nseg)                                 \
                : launch_screen_t<PREC, NKS, NB, VEC, TX, false>(             \

@@ -6,7 +6,7 @@
 #   diag      tools/c3_diag.py on the main library and on libdkm_old.so
 #   c3it      C3 bench line under a rocprofv3 kernel trace, per iteration
 #   c4it      C4 bench line under a rocprofv3 kernel trace, per iteration
-#   c3ab      C3 bench line, main vs libdkm_old.so, two rounds
+#   c3ab      C3 bench line, main vs libdkm_$AB.so (default old), two rounds
 #   c2ab      C2 headline line, main vs libdkm_$AB.so (AB env, default w32pf2), two rounds
 #   bench     default bench.py
 TAG=${1:-r05}; shift
@@ -47,8 +47,8 @@ for s in "$@"; do
       step c4it 400 rocprofv3 --kernel-trace --stats -d $P -o run -- $C4
       DB=$(find $P -name "*.db" | head -1); [ -n "$DB" ] && python tools/prof_iters.py $DB > $P/iters.txt 2>&1 && rm -f $DB; find $P -type f ! -name iters.txt -delete
       cut -c1-400 $P/iters.txt ;;
-    c3ab) for r in 1 2; do for v in main old; do
-        if [ $v = old ]; then export DKM_LIB=$OLD; else unset DKM_LIB; fi
+    c3ab) V=${AB:-old}; for r in 1 2; do for v in main $V; do
+        if [ $v = main ]; then unset DKM_LIB; else export DKM_LIB=$PWD/dislib_amd/libdkm_$v.so; fi
         step c3_$v$r 300 $C3
         python -c "import json;d=json.loads([l for l in open('$OUT/${TAG}_c3_$v$r.log') if l.startswith('{')][-1]);print('$v', round(d['ms_per_step'],3), 'fit', round(d['fit_ms_per_iter'],2), 'kern', round(d['roofline']['kernel_ms'],3))"
       done; done; unset DKM_LIB ;;
