@@ -34,8 +34,12 @@ def _freeze(x):
     """Make a host sample array (or a CSR matrix's arrays) read-only: the
     HBM copy is its image, so an in-place edit must fail loudly instead of
     leaving later fits on stale device data (the reference re-reads the
-    samples on every task).  Assign a new array to change a Subset's
-    samples; that re-uploads."""
+    samples on every task).  A visible side effect on caller-owned arrays,
+    documented on ``Dataset``; assign a new array to change a Subset's
+    samples, which re-uploads.  When the samples are a view (``x.base`` is
+    an array, e.g. the slices ``load_data`` makes of the caller's matrix),
+    only the view is frozen: the caller's own matrix stays writable, and a
+    write through it is not caught (``Dataset`` says so)."""
     if isinstance(x, np.ndarray):
         x.setflags(write=False)
     elif issparse(x):
@@ -132,7 +136,19 @@ class Subset(object):
 
 
 class Dataset(object):
-    """Ordered list of Subsets.  Reference: ``data/classes.py:8-277``."""
+    """Ordered list of Subsets.  Reference: ``data/classes.py:8-277``.
+
+    Device residency: the first device use (a fit, a predict, a neighbour
+    query) uploads the samples to HBM and keeps them there.  From then on
+    the host arrays behind it -- each Subset's ``samples`` ndarray and the
+    arrays of a CSR matrix -- are made read-only, so that an in-place write fails loudly instead of leaving
+    the device copy stale (the reference re-reads samples on every task).
+    To change the data, assign new arrays to the Subsets (``ds[i].samples
+    = new``); the next device use uploads them.  Device tensors given as
+    samples are tracked by their version counter instead.  Not caught: a
+    write through an array the samples are views of (``load_data(x)``
+    slices ``x``; ``x`` itself stays writable) -- treat such an array as
+    read-only while the Dataset is in use, or pass a copy."""
 
     def __init__(self, n_features, sparse=False):
         self._subsets = list()
