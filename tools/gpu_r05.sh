@@ -52,7 +52,7 @@ for s in "$@"; do
         step c3_$v$r 300 $C3
         python -c "import json;d=json.loads([l for l in open('$OUT/${TAG}_c3_$v$r.log') if l.startswith('{')][-1]);print('$v', round(d['ms_per_step'],3), 'fit', round(d['fit_ms_per_iter'],2), 'kern', round(d['roofline']['kernel_ms'],3))"
       done; done; unset DKM_LIB ;;
-    c2ab) V=${AB:-w32pf2}; for r in 1 2; do for v in main $V; do
+    c2ab) for r in 1 2; do for v in main ${AB:-w32pf2}; do
         if [ $v = main ]; then unset DKM_LIB; else export DKM_LIB=$PWD/dislib_amd/libdkm_$v.so; fi
         step c2_$v$r 300 python bench.py --steps 20 --warmup 3 --no-cpu --only-headline
         python -c "import json;d=json.loads([l for l in open('$OUT/${TAG}_c2_$v$r.log') if l.startswith('{')][-1]);print('$v', round(d['ms_per_step'],3), 'fit', round(d['fit_ms_per_iter'],2), 'kern', round(d['roofline']['kernel_ms'],3))"
