@@ -208,8 +208,12 @@ __global__ void k_gemm_cnorm(const float *__restrict__ cn32, int64_t k,
 __global__ void __launch_bounds__(GTHREADS)
     k_gemm_screen3(const char *__restrict__ afrag, const float *__restrict__ gcn,
                   const char *__restrict__ xs, int nst, int nct, int nks,
-                  int2 *__restrict__ part) {
+                  int2 *__restrict__ part, uint32_t *__restrict__ gcount) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  // the merge's candidate-list counter, reset for this chunk (the previous
+  // chunk's readers ran before this launch on the stream; a memset launch
+  // per chunk cost 0.8 ms per C4 iteration)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *gcount = 0;
   typedef __attribute__((address_space(3))) void lds_void;
   // XCD-aware bijective remap (blocks b and b + 8 share an XCD): the nct
   // centre tiles of one sample tile run on one XCD, so its split rows are
@@ -423,9 +427,11 @@ constexpr int G1LDS = G1NRM + 2 * GT * 4;
 __global__ void __launch_bounds__(GTHREADS)
     k_gemm_screen1(const char *__restrict__ afrag,
                    const float *__restrict__ gcn, const char *__restrict__ xs,
-                   int nst, int nct, int nks, int2 *__restrict__ part) {
+                   int nst, int nct, int nks, int2 *__restrict__ part,
+                   uint32_t *__restrict__ gcount) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   typedef __attribute__((address_space(3))) void lds_void;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *gcount = 0;  // as k_gemm_screen3
   const int G = nst * nct;
   const int per = (int)(gridDim.x >> 3);  // workgroups per XCD
   const int xcd = (int)(blockIdx.x & 7), j = (int)(blockIdx.x >> 3);
@@ -1172,14 +1178,12 @@ int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
       const int64_t G = (int64_t)nst * nct;
       const int64_t nwg = 8 * std::min<int64_t>(ss.cus / 8, (G + 7) / 8);
       k_gemm_screen1<<<(unsigned)nwg, GTHREADS, G1LDS, s>>>(
-          v.gfrag1, v.gcn, xs, nst, nct, nks, v.gpart);
+          v.gfrag1, v.gcn, xs, nst, nct, nks, v.gpart, &v.hdr->gcount);
     } else {
       k_gemm_screen3<<<(unsigned)(nst * nct), GTHREADS, GLDS, s>>>(
-          v.gfrag, v.gcn, xs, nst, nct, nks, v.gpart);
+          v.gfrag, v.gcn, xs, nst, nct, nks, v.gpart, &v.hdr->gcount);
     }
     if (int r = check_launch("gemm screen")) return r;
-    if (hipMemsetAsync(&v.hdr->gcount, 0, 4, s) != hipSuccess)
-      return fail(DKM_E_LAUNCH, "gemm: list reset");
     const unsigned mb = (unsigned)std::min<int64_t>((rows + 255) / 256, 8192);
     k_gemm_merge<TX><<<mb, 256, 0, s>>>(X, c0, rows, d, ldx, k, nct, dpad,
                                         v.gpart, xn, vb, lab_out, acc, flags,
