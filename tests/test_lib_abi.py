@@ -61,3 +61,23 @@ def test_constants_match_header():
     assert int(consts["DKM_SUMS_F32"]) == _lib.SUMS_F32
     assert int(consts["DKM_SUMS_RECIP"]) == _lib.SUMS_RECIP
     assert int(consts["DKM_PREP_CSR"]) == _lib.PREP_CSR
+
+
+def test_knn_workspace_covers_both_paths():
+    """kNN beyond 32 neighbours takes the two-scan path (32 < kn <= 2048)
+    and reruns in passes of 32 when a candidate list overflows, so its
+    workspace covers both; beyond 2048 only the passes'.  Host-only."""
+    so = _lib.load()
+    passes = so.dkm_knn_workspace_bytes(5000, 100000, 32)
+    assert passes > 0
+    for kn in (33, 1000, 2048):
+        two = so.dkm_knn_workspace_bytes(5000, 100000, kn)
+        assert two >= passes
+        # the two-scan chunk: per query the candidate cap (4096 x 12 B)
+        assert two >= 5000 * 4096 * 12
+    assert so.dkm_knn_workspace_bytes(5000, 100000, 2049) < \
+        so.dkm_knn_workspace_bytes(5000, 100000, 2048)
+    # queries past the 8192-query chunk reuse its workspace
+    big = so.dkm_knn_workspace_bytes(100000, 100000, 1000)
+    assert big < 100000 * 4096 * 12
+    assert so.dkm_knn_workspace_bytes(10, 5, 6) == 0   # kn > nx
