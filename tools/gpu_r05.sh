@@ -3,7 +3,8 @@
 # crash / timeout / fault stops the session).  usage: gpu_r05.sh TAG STEP...
 #   t_sorted  sorted-image / b2 / C3 full-size label tests
 #   t_all     the whole GPU suite
-#   diag      tools/c3_diag.py on the main library and on libdkm_old.so
+#   diag      tools/c3_diag.py on the main library (and libdkm_old.so when built:
+#             bash dislib_amd/csrc/variants_b2.sh old -DDKM_AB_NO_SORTED_FAST=1 dkm_b2)
 #   c3it      C3 bench line under a rocprofv3 kernel trace, per iteration
 #   c4it      C4 bench line under a rocprofv3 kernel trace, per iteration
 #   c3ab      C3 bench line, main vs libdkm_$AB.so (default old), two rounds
@@ -30,7 +31,7 @@ for s in "$@"; do
     t_sorted) step t_sorted 900 $PT tests/test_gpu_sorted.py tests/test_gpu_b2.py tests/test_gpu_fullsize.py::test_c3_full_size_labels ;;
     t_all) step t_all 1100 $PT -m gpu tests ;;
     diag) step diag_main 240 python tools/c3_diag.py
-          DKM_LIB=$OLD step diag_old 240 python tools/c3_diag.py ;;
+          [ -f $OLD ] && DKM_LIB=$OLD step diag_old 240 python tools/c3_diag.py ;;
     c3it) P=$OUT/${TAG}_c3it; mkdir -p $P
       step c3it 300 rocprofv3 --kernel-trace --stats -d $P -o run -- $C3
       DB=$(find $P -name '*.db' | head -1)
