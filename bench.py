@@ -11,17 +11,23 @@ fused assign + per-cluster sum/count (HIP) -> all-reduce of [sums | counts]
 (RCCL through libdkm, N > 1) -> centre update + convergence criterion
 (HIP) -> 4-byte flag read.  Weak scaling: every rank owns n samples.
 
+Timing follows SURVEY 8(d): W warmup iterations run on a throwaway fit;
+the K timed steps are ONE whole fit from the initial centres (iteration 0,
+the image builds and the mass migration of iterations 1-2 included; tol =
+0, so exactly K iterations), bracketed by barrier + synchronize.  `value` =
+n x N x K / that wall time.  The steady-state figures (the fit's last
+ceil(K/2) iterations) are reported beside it, never as `value`.
+
 Prints ONE JSON line (rank 0): metric/value/unit for the headline config,
 its roofline (the assignment call -- the dominant kernels -- timed with HIP
-events on its stream), a CPU baseline (the oracle on this host, rank 0,
-N=1 only, bounded sample), the fit_predict variant (labels written), and
-under "extra_configs" the other single-GPU BASELINE configs measured the
-same way in the same run: configs[2]'s per-GPU shard (125M x 64, k=1000,
-the north-star target), configs[3] (10M x 1024, k=4096, fp64 and fp32;
-MFMA) and configs[4] (CSR 10M x 10k, 10 entries per row, k=256: fit and
-predict).  Every line also carries the whole-fit figure:
-the W + K iterations from the initial centres, iteration 0 included,
-tol = 0.
+events on its stream over the timed fit, and over its steady iterations),
+a CPU baseline (the oracle on this host, rank 0, N=1 only, bounded sample),
+the fit_predict variant (labels written), per-iteration wall and kernel
+times, and under "extra_configs" the other single-GPU BASELINE configs
+measured the same way in the same run: configs[0] (C1), configs[2]'s
+per-GPU shard (125M x 64, k=1000, the north-star target), configs[3] (10M
+x 1024, k=4096, fp64 and fp32; MFMA) and configs[4] (CSR 10M x 10k, 10
+entries per row, k=256: fit and predict).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--only-headline]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -191,19 +197,29 @@ def _cpu_task(block, centers, sparse=False):
 # ---------------------------------------------------------------------------
 def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
                mode, labels, n_blobs=None, f32=False, csr_nnz=0, host_x=None):
-    """One configuration: a fresh fit state, W warmup iterations, then
-    exactly K timed iterations (barrier + synchronize on both sides).
-    The fit starts at iteration 0 (initial centres, the most expensive
-    step), so warmup + timed iterations are one whole fit of W + K
-    iterations with tol = 0: its wall time (barrier waits excluded) is the
-    SURVEY 8(d) whole-loop figure, from the initialised centres through the
-    last convergence decision."""
+    """One configuration, timed as SURVEY 8(d) defines the metric: the wall
+    time of a whole Lloyd loop, from after the data is resident and the
+    centres are initialised through the last convergence decision.
+
+    * W warmup iterations of a throwaway fit on the same resident data (code
+      objects, allocator); its sample images are then dropped, so the timed
+      fit builds every image it uses, as a first fit on a dataset does;
+    * the timed fit: a fresh fit state from the initial centres, then exactly
+      K iterations with tol = 0 (barrier + synchronize on both sides), so
+      iteration 0 -- the most expensive one -- is inside the timed region;
+    * per iteration: HIP events around the assignment call (the dominant
+      kernels, on their stream) and the host clock after the iteration's
+      flag read (the per-iteration sync), so every iteration's wall time and
+      kernel time are reported; the "steady" figures are the last ceil(K/2)
+      iterations of the same fit;
+    * every workspace / image allocation's host time (_device.ALLOC_LOG)."""
     progress("gpu n=%d d=%d k=%d steps=%d warmup=%d%s" % (
         n, d, k, steps, warmup, " csr" if csr_nnz else ""))
     from dislib_amd import _device, _shard
     from dislib_amd.cluster.kmeans import _Lloyd, _init_centers
     from dislib_amd.data import Dataset, Subset
     n_blobs = n_blobs or k
+    tp0 = time.perf_counter()
     if host_x is not None:
         # C1: the reference's own make_blobs (host numpy), rank's slice
         X = torch.from_numpy(np.ascontiguousarray(
@@ -223,20 +239,33 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
     ds = Dataset(n_features=d, sparse=bool(csr_nnz))
     for i in range(0, n, subset):
         ds.append(Subset(X[i:i + subset]))
-    ds._device_data(dev)                  # resident before the fit starts
+    dd = ds._device_data(dev)             # resident before the fit starts
+    torch.cuda.synchronize()
+    phases = {"data_s": time.perf_counter() - tp0}
+    del _device.ALLOC_LOG[:]
+    # warmup: a throwaway fit of W iterations
+    tw = time.perf_counter()
+    if warmup > 0:
+        st = _Lloyd(ds, C0, 0.0, labels, mode, dev)
+        for _ in range(warmup):
+            st.step()
+        torch.cuda.synchronize()
+        del st
+    dd.drop_images()
+    phases["warmup_fit_s"] = time.perf_counter() - tw
+    ts = time.perf_counter()
     st = _Lloyd(ds, C0, 0.0, labels, mode, dev)
     torch.cuda.synchronize()
-    tf = time.perf_counter()
-    for _ in range(warmup):
-        st.step()
-    torch.cuda.synchronize()
-    warm_s = time.perf_counter() - tf
+    phases["fit_state_s"] = time.perf_counter() - ts
     ev = [(torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    wall = []
+    nlog = len(_device.ALLOC_LOG)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    tl = t0
     for i in range(steps):
         st.prepare()
         ev[i][0].record()
@@ -244,11 +273,22 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
         ev[i][1].record()
         st.reduce_update()
         st.read_flags()               # the per-iteration convergence read
+        tn = time.perf_counter()
+        wall.append(tn - tl)
+        tl = tn
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kern = [s.elapsed_time(e) for s, e in ev]
+    ns = (steps + 1) // 2                 # the steady iterations: the last half
+    kern_ms = float(np.mean(kern))
+    steady_kern_ms = float(np.mean(kern[-ns:]))
+    steady_ms = float(np.mean(wall[-ns:])) * 1e3
+    phases["fit_allocs"] = [{"what": w, "bytes": b, "s": round(s, 6)}
+                            for w, b, s in _device.ALLOC_LOG[nlog:]]
+    phases["warmup_allocs_s"] = round(sum(s for _, _, s in
+                                          _device.ALLOC_LOG[:nlog]), 6)
     pred_ms = None
     if csr_nnz:                       # predict on the final centres
         from dislib_amd import _lib
@@ -262,13 +302,16 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
         pred_ms = (time.perf_counter() - tp) / 3 * 1e3
         del lab
     if world > 1:
-        t = torch.tensor([el, kern_ms, warm_s], dtype=torch.float64,
-                         device=dev)
+        t = torch.tensor([el, kern_ms, steady_kern_ms, steady_ms],
+                         dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, kern_ms, warm_s = float(t[0]), float(t[1]), float(t[2])
+        el, kern_ms, steady_kern_ms, steady_ms = (float(x) for x in t)
     info = _shard.comm_info(dev.index) if world > 1 else None
-    out = {"el": el, "kern_ms": kern_ms, "rechecked": st.rechecked(),
-           "fit_s": warm_s + el, "fit_iters": warmup + steps,
+    out = {"el": el, "kern_ms": kern_ms, "steady_kern_ms": steady_kern_ms,
+           "steady_ms": steady_ms, "steady_iters": ns,
+           "iter_ms": [round(w * 1e3, 3) for w in wall],
+           "iter_kern_ms": [round(x, 3) for x in kern],
+           "phases": phases, "rechecked": st.rechecked(),
            "pred_ms": pred_ms,
            "collective": ("libdkm-rccl" if info else "torch.distributed")
            if world > 1 else "none",
@@ -282,7 +325,7 @@ def run_config(torch, dist, dev, rank, world, n, d, k, subset, steps, warmup,
            "counters": st.screened_blocks() if not csr_nnz and
            getattr(st, "sorting", False) else None,
            "nkb": (k + 31) // 32}
-    del st, ds, X
+    del st, ds, X, dd
     torch.cuda.empty_cache()
     return out
 
@@ -318,11 +361,15 @@ def skip_fields(r):
 
 
 def fit_fields(r, n, world):
-    """The whole-fit figure of a run: W + K iterations from
-    the initial centres, tol = 0."""
-    return {"fit_iters": r["fit_iters"], "fit_s": r["fit_s"],
-            "fit_ms_per_iter": r["fit_s"] / r["fit_iters"] * 1e3,
-            "fit_value": n * world * r["fit_iters"] / r["fit_s"]}
+    """Per-iteration record of the timed fit (K iterations from
+    the initial centres, tol = 0): wall time per iteration (host clock after
+    each flag read), assignment-kernel time per iteration (HIP events), the
+    steady figure (the fit's last ceil(K/2) iterations) and the host-side
+    phases (data generation, warmup fit, fit-state setup, allocations)."""
+    return {"iter_ms": r["iter_ms"], "iter_kernel_ms": r["iter_kern_ms"],
+            "steady_ms_per_step": r["steady_ms"],
+            "steady_value": n * world / (r["steady_ms"] * 1e-3),
+            "phases": r["phases"]}
 
 
 def screen_products(k, d):
@@ -335,35 +382,46 @@ def screen_products(k, d):
     return 3 if frags + (k * lds_stride + k) * 8 <= 80 * 1024 else 1
 
 
-def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
-    """Roofline of the assignment call (the dominant kernels).  Small d:
-    HBM-bound, algorithmic bytes = the X read (es d per sample, SURVEY
-    8(d)).  d > 128: MFMA-bound, the
-    executed MFMA flops of the single-product GEMM screen (2 k d per sample
-    over the padded tiles) against the dense bf16 peak.  CSR (C5): the HBM
-    bytes of the rows (12 B per stored entry + 8 B of indptr) and labels;
-    its real limit is the gather of fp32 centre columns from L2 (4 B per
-    stored entry and centre), reported beside it."""
+def roofline(n, d, k, r, labels, es=8, csr_nnz=0, traffic=None):
+    """Roofline of the assignment call (the dominant kernels), timed with
+    HIP events on its stream over the timed fit (`kernel_ms`: the mean over
+    its K iterations, iteration 0 included -- the SURVEY 8(d) loop), with
+    `step_frac` the same work over the fit's wall time per iteration and
+    `steady` the same figures over the fit's last ceil(K/2) iterations.
+
+    * d <= 128: HBM-bound on the algorithmic bytes, the X read (es d per
+      sample, SURVEY 8(d));
+    * d > 128: MFMA-bound, the executed flops of the single-product GEMM
+      screen (2 k d per sample over the padded tiles) against the dense bf16
+      peak;
+    * CSR (C5): the HBM bytes of the rows (12 B per stored entry + 8 B of
+      indptr + 8 B of labels); the gather of bf16 centre columns from L2
+      (2 B per stored entry and centre) beside it.
+    `traffic` (PMC bytes per steady launch, profiles/traffic/) gives
+    `steady.physical`."""
     sec = r["kern_ms"] * 1e-3
+    step_sec = r["el"] / len(r["iter_ms"])
+    st_sec = r["steady_kern_ms"] * 1e-3
+    st_step = r["steady_ms"] * 1e-3
     if csr_nnz:
-        b = n * (12 * csr_nnz + 8 + 8)
-        g = n * csr_nnz * k * 4
-        out = {"bound": "hbm", "achieved": b / sec / 1e9,
-               "peak": HBM_PEAK_GBS, "unit": "GB/s",
-               "frac": b / sec / 1e9 / HBM_PEAK_GBS,
+        work = n * (12 * csr_nnz + 8 + 8)
+        g = n * csr_nnz * k * 2
+        out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
                "bytes_per_sample": 12 * csr_nnz + 16,
-               "kernel": "dkm_assign_delta_csr / dkm_partial_sum_csr (slice "
-                         "screen + merge + resolve)",
-               "kernel_ms": r["kern_ms"],
-               "l2_gather": {"bytes_per_sample": csr_nnz * k * 4,
-                             "achieved_tbs": g / sec / 1e12,
+               "kernel": "dkm_assign_delta_csr / dkm_partial_sum_csr (screen "
+                         "+ merge + resolve)",
+               "l2_gather": {"bytes_per_sample": csr_nnz * k * 2,
+                             "table": "bf16 C^T (d x k)",
+                             "achieved_tbs": g / st_sec / 1e12,
                              "peak_tbs": L2_PEAK_TBS,
-                             "frac": g / sec / 1e12 / L2_PEAK_TBS}}
+                             "frac": g / st_sec / 1e12 / L2_PEAK_TBS,
+                             "note": "steady launches"}}
+        scale, peak = 1e9, HBM_PEAK_GBS
     elif d <= 128:
         # SURVEY 8(d): the fit streams X once per iteration, es * d bytes
         # per sample (the labels the delta path reads and writes are not
         # counted)
-        b = n * es * d
+        work = n * es * d
         ik = r.get("image_kind", 0)
         # bytes the screen actually streams per sample: the resident bf16
         # image (SPLIT: hi + lo, 4 KB per 32-row tile; SINGLE: 1 KB per
@@ -376,77 +434,90 @@ def roofline(n, d, k, r, labels, es=8, csr_nnz=0):
             sb = (d + 15) // 16 * 1024 // 32 + 4 + 8 + 4
         else:
             sb = es * d + 8
-        out = {"bound": "hbm", "achieved": b / sec / 1e9,
-               "peak": HBM_PEAK_GBS, "unit": "GB/s",
-               "frac": b / sec / 1e9 / HBM_PEAK_GBS,
+        out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
                "bytes_per_sample": es * d,
                "kernel": "dkm_assign_delta / dkm_partial_sum (screen + "
-                         "re-check)",
-               "kernel_ms": r["kern_ms"],
-               # MFMA products per x.c term of the screen auto mode picks:
-               # bf16x3 (3) when the fp64 sums fit LDS beside the centre
-               # fragments, else the single-product screen (1)
+                         "re-check + sums)",
+               # MFMA products per x.c term of the steady screen: bf16x3 (3)
+               # when the fp64 sums fit LDS beside the centre fragments,
+               # else the single-product screen (1)
                "mfma_products": screen_products(k, d),
-               "mfma_bf16_tflops_executed":
-                   2.0 * screen_products(k, d) * k * d * n / sec / 1e12,
-               "mfma_bf16_peak_tflops": BF16_PEAK_TFLOPS,
                "image": {0: "none (X converted in the screen)",
                          1: "bf16 single (resident, built in the fit)",
                          2: "bf16 hi+lo split (resident, built in the "
                             "fit)",
                          3: "bf16 single, rows grouped by label (built in "
                             "the fit; block skipping)"}[ik],
-               "streamed_bytes_per_sample": sb,
-               "streamed_gbs": n * sb / sec / 1e9,
-               "streamed_frac": n * sb / sec / 1e9 / HBM_PEAK_GBS}
+               "streamed_bytes_per_sample": sb}
+        scale, peak = 1e9, HBM_PEAK_GBS
     else:
         # auto mode runs the single-product GEMM screen (bf16 hi x hi on
-        # hi-only tiles, features padded to 32)
+        # hi-only tiles, features padded to 32) in the steady iterations
         dp, kp = (d + 31) // 32 * 32, (k + 255) // 256 * 256
-        f = 2.0 * kp * dp * n
-        out = {"bound": "mfma", "achieved": f / sec / 1e12,
-               "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-               "frac": f / sec / 1e12 / BF16_PEAK_TFLOPS,
+        work = 2.0 * kp * dp * n
+        out = {"bound": "mfma", "unit": "TFLOP/s", "peak": BF16_PEAK_TFLOPS,
+               "flops_per_sample": 2.0 * kp * dp,
                "kernel": "dkm_assign (single-product bf16 GEMM screen + "
                          "exact candidates + sums)",
                "mfma_products": 1,
-               "kernel_ms": r["kern_ms"],
-               "alg_fp64_equiv_tflops": 2.0 * k * d * n / sec / 1e12,
-               "fp64_peak_tflops": FP64_PEAK_TFLOPS,
-               "hbm_gbs": n * es * d / sec / 1e9,
                "image": ("bf16 GEMM tiles (resident, built in the fit)"
                          if r.get("image_kind", 0) == 4 else
                          "none (X split per chunk on a second stream)")}
-    out["traffic"] = None
+        scale, peak = 1e12, BF16_PEAK_TFLOPS
+
+    def rate(s):
+        return work / s / scale
+
+    out.update({"achieved": rate(sec), "frac": rate(sec) / peak,
+                "kernel_ms": r["kern_ms"],
+                "step_frac": rate(step_sec) / peak,
+                "timed": "mean over the K iterations of the timed fit "
+                         "(iteration 0 included)"})
+    st = {"iterations": r["steady_iters"], "kernel_ms": r["steady_kern_ms"],
+          "achieved": rate(st_sec), "frac": rate(st_sec) / peak,
+          "ms_per_step": r["steady_ms"], "step_frac": rate(st_step) / peak}
+    if traffic:
+        st["physical"] = {"hbm_bytes_per_sample": traffic / n,
+                          "achieved_gbs": traffic / st_sec / 1e9,
+                          "frac": traffic / st_sec / 1e9 / HBM_PEAK_GBS,
+                          "note": "PMC FETCH_SIZE x2 + WRITE_SIZE (gfx950 "
+                                  "correction) per steady launch, "
+                                  "profiles/traffic/"}
+    if d <= 128 and not csr_nnz:
+        ik = out["streamed_bytes_per_sample"]
+        st["streamed_gbs"] = n * ik / st_sec / 1e9
+        st["streamed_frac"] = n * ik / st_sec / 1e9 / HBM_PEAK_GBS
+        st["mfma_bf16_tflops_executed"] = \
+            2.0 * screen_products(k, d) * k * d * n / st_sec / 1e12
+    out["steady"] = st
+    out["traffic"] = traffic
     out["binding"] = binding_for(d, k, csr_nnz)
     return out
 
 
 def binding_for(d, k, csr_nnz):
-    """The resource that actually limits the dominant kernel, from the PMC
-    passes committed under profiles/ (DESIGN.md 5): the algorithmic `frac`
-    prices fp64 X bytes or executed MFMA flops, which the screens that read
-    a resident bf16 image do not stream."""
+    """The resource that actually limits the steady dominant kernel, from
+    the PMC passes committed under profiles/ (DESIGN.md 5): the algorithmic
+    `frac` prices fp64 X bytes or executed MFMA flops, which the screens
+    that read a resident bf16 image do not stream."""
     if csr_nnz:
-        return ("L2 gather of the fp32 centre columns (4 B per stored entry "
-                "and centre; not HBM)")
+        return ("latency of the bf16 C^T gathers: k_csr_screen waits "
+                "(SQ_WAIT_ANY) 70% of its wave cycles at 8 waves per SIMD "
+                "with 96% L2 hits; neither HBM nor L2 bandwidth saturates "
+                "(profiles/r05/pmc/c5_csr_pmc_summary_10M_bf16.txt)")
     if d > 128:
-        return "MFMA issue of the single-product bf16 GEMM screen"
-    return ("instruction issue (VALU + MFMA of the screen: neither the HBM "
-            "stream of the bf16 image nor the MFMA pipe saturates; "
-            "see `physical` and profiles/r04/pmc)")
-
-
-def physical(rf, n, sec):
-    """The HBM bytes the assignment kernels really move (PMC traffic per
-    launch) against the 8 TB/s peak, beside the algorithmic `frac`."""
-    tb = rf.get("traffic")
-    if not tb:
-        return None
-    return {"hbm_bytes_per_sample": tb / n, "achieved_gbs": tb / sec / 1e9,
-            "frac": tb / sec / 1e9 / HBM_PEAK_GBS,
-            "note": "PMC FETCH_SIZE x2 + WRITE_SIZE (gfx950 correction), "
-                    "profiles/traffic/"}
+        return ("the LDS-read + MFMA loop of k_gemm_screen1: 2 waves per "
+                "SIMD, SQ_WAIT_INST_ANY 38% of wave cycles, 1.7x the "
+                "algorithmic HBM bytes "
+                "(profiles/r05/pmc/c4_pmc_summary_10M.txt)")
+    if k * d > 32 * 128:
+        return ("instruction issue of k_screen_sorted over the label-sorted "
+                "image: VALU:MFMA 7.4:1, 45% MFMA busy, SQ_WAIT_ANY 35% "
+                "(profiles/r05/pmc/c3_sorted_pmc_summary_20M_r05z.txt)")
+    return ("instruction issue of k_screen_w32 over the split image: "
+            "VALU:MFMA 13.4:1, SQ_WAIT_ANY 35% at 3 waves per SIMD; the "
+            "image stream runs at about half of HBM "
+            "(profiles/r05/pmc/c2_pmc_summary_20M.txt)")
 
 
 def main():
@@ -456,22 +527,24 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     sc = a.extras_scale
     extras = [] if a.only_headline else [
-        # (name, n, d, k, subset, steps, warmup, fp32 samples, csr nnz/row)
+        # (name, n, d, k, subset, steps, warmup, fp32 samples, csr nnz/row);
+        # steps = the SURVEY 8(d) iteration count of the config (C1 10, C3
+        # 10, C4 5, C5 5): the timed fit is that whole Lloyd loop
         ("KMeans k=10 on 100k x 50 fp64 make_blobs per GPU (BASELINE "
          "configs[0], the reference's CPU-runnable parity case)", 100_000,
-         50, 10, 10_000, 8, 2, False, "c1"),
+         50, 10, 10_000, 10, 2, False, "c1"),
         ("KMeans k=1000 on 125M x 64 fp64 dense per GPU (BASELINE "
          "configs[2] per-GPU shard; north-star target)",
-         125_000_000, 64, 1000, 1_000_000, 8, 2, False, 0),
+         125_000_000, 64, 1000, 1_000_000, 10, 2, False, 0),
         ("KMeans k=4096 on 10M x 1024 fp64 dense per GPU (BASELINE "
-         "configs[3], MFMA-bound)", 10_000_000, 1024, 4096, 1_000_000, 4, 2,
+         "configs[3], MFMA-bound)", 10_000_000, 1024, 4096, 1_000_000, 5, 1,
          False, 0),
         ("KMeans k=4096 on 10M x 1024 fp32 dense per GPU (BASELINE "
          "configs[3], fp32 variant reported separately)", 10_000_000, 1024,
-         4096, 1_000_000, 4, 2, True, 0),
+         4096, 1_000_000, 5, 1, True, 0),
         ("KMeans k=256 on sparse CSR 10M x 10k at 0.1% density per GPU "
          "(BASELINE configs[4], fit + predict)", 10_000_000, 10_000, 256,
-         1_000_000, 4, 1, False, 10),
+         1_000_000, 5, 1, False, 10),
     ]
 
     # CPU baselines first, before anything touches the GPU: their worker
@@ -543,14 +616,11 @@ def main():
              "value": n * world * steps / rr["el"],
              "unit": "samples·iters/s", "ms_per_step": rr["el"] / steps * 1e3,
              "steps": steps, "warmup": warm,
-             "roofline": dict(roofline(n, d, k, rr, False, 4 if f32 else 8,
-                                       csr_nnz=nnz),
-                              traffic=None if f32 else
-                              traffic_for(n, d, k, csr_nnz=nnz)),
+             "roofline": roofline(n, d, k, rr, False, 4 if f32 else 8,
+                                  csr_nnz=nnz, traffic=None if f32 else
+                                  traffic_for(n, d, k, csr_nnz=nnz)),
              "rechecked_samples": rr["rechecked"],
              "block_skip": skip_fields(rr)}
-        e["roofline"]["physical"] = physical(e["roofline"], n,
-                                             rr["kern_ms"] * 1e-3)
         e.update(fit_fields(rr, n, world))
         if nnz:
             e["nnz_per_row"] = nnz
@@ -577,9 +647,8 @@ def main():
         return
 
     value = a.n * world * a.steps / r["el"]
-    rf = roofline(a.n, a.d, a.k, r, a.labels)
-    rf["traffic"] = traffic_for(a.n, a.d, a.k, a.traffic_json)
-    rf["physical"] = physical(rf, a.n, r["kern_ms"] * 1e-3)
+    rf = roofline(a.n, a.d, a.k, r, a.labels,
+                  traffic=traffic_for(a.n, a.d, a.k, a.traffic_json))
     out = {
         "metric": METRIC,
         "value": value,
@@ -594,8 +663,10 @@ def main():
         "dtype": "f64",
         "data": "synthetic (on-device counter-based make_blobs, k blobs)",
         "config": {"workload": "KMeans k=%d on %dM x %d fp64 dense per GPU "
-                               "(BASELINE configs[1])" % (a.k, a.n // 10**6,
-                                                          a.d),
+                               "(BASELINE configs[1]); timed = one whole "
+                               "Lloyd loop of `steps` iterations from the "
+                               "initial centres, tol = 0 (SURVEY 8(d))" % (
+                                   a.k, a.n // 10**6, a.d),
                    "n_per_gpu": a.n, "d": a.d, "k": a.k,
                    "subset_size": a.subset, "mode": a.mode,
                    "labels": bool(a.labels),

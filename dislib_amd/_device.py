@@ -22,6 +22,17 @@ from . import _lib
 X_IMAGE = True
 # HBM left free after an image is allocated
 _IMAGE_HEADROOM = 4 << 30
+# (what, bytes, host seconds) of every workspace / image allocation: lets a
+# caller (bench.py) attribute host time inside a fit to its allocations
+ALLOC_LOG = []
+
+
+def _alloc(what, nbytes, fn):
+    import time
+    t0 = time.perf_counter()
+    out = fn()
+    ALLOC_LOG.append((what, int(nbytes), time.perf_counter() - t0))
+    return out
 
 
 def torch():
@@ -149,7 +160,8 @@ class DeviceData:
         if nb == 0 or nb + _IMAGE_HEADROOM > free:
             self._image_failed.add(kind)
             return None, 0
-        img = t.empty(nb, dtype=t.uint8, device=self.device)
+        img = _alloc("image%d" % kind, nb, lambda: t.empty(
+            nb, dtype=t.uint8, device=self.device))
         fn = so.dkm_x_image_f32 if self.dtype == np.float32 else \
             so.dkm_x_image_f64
         _lib.check(fn(ptr(self.X), self.n, self.d, self.X.stride(0), kind,
@@ -221,7 +233,8 @@ class Workspace:
                                                  int(n_queue)))
         if self.nbytes == 0:
             raise _lib.DkmError("dkm_workspace_bytes: bad k/d")
-        self.buf = t.zeros(self.nbytes, dtype=t.uint8, device=device)
+        self.buf = _alloc("workspace", self.nbytes, lambda: t.zeros(
+            self.nbytes, dtype=t.uint8, device=device))
         preload(self.buf.device)
 
     @property
@@ -353,7 +366,8 @@ def sorted_image(dd, labels, k, ws, old=None, acc=None):
         free = t.cuda.mem_get_info(dd.device)[0]
         if nb == 0 or nb + _IMAGE_HEADROOM > free:
             return None, 0
-        img = t.empty(nb, dtype=t.uint8, device=dd.device)
+        img = _alloc("image_sorted", nb, lambda: t.empty(
+            nb, dtype=t.uint8, device=dd.device))
     if int(so.dkm_workspace_bytes(int(k), dd.d, dd.n)) > ws.nbytes:
         return None, 0
     f32 = dd.dtype == np.float32

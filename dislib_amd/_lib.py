@@ -11,7 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DKM_LIB", os.path.join(_HERE, "libdkm.so"))
 
 # constants mirrored from include/dkm.h
-ABI_VERSION = 2
+ABI_VERSION = 3
 MODE_AUTO, MODE_EXACT, MODE_SCREEN32, MODE_BF16X3, MODE_BF16 = 0, 1, 2, 3, 4
 MODE_MASK, MODE_NOHINT, MODE_B1 = 0xff, 0x100, 0x200
 IMAGE_NONE, IMAGE_SINGLE, IMAGE_SPLIT, IMAGE_SORTED, IMAGE_GEMM = 0, 1, 2, 3, 4

@@ -1548,6 +1548,7 @@ template int launch_screen_b2<float>(const float *, int64_t, int, int64_t, int,
 // Code-object preload (dkm_preload): the runtime loads this file's kernels
 // on first use of any of them; an attribute query here does it up front.
 namespace dkm {
+DKM_TU_FLAGS(b2, DKM_AB_B2_PROBE)
 __global__ void k_tu_b2() {}
 int preload_b2() {
   hipFuncAttributes a;

@@ -118,6 +118,7 @@ template int launch_cand2_leaf<float>(const float *, int, int64_t,
 // Code-object preload (dkm_preload): the runtime loads this file's kernels
 // on first use of any of them; an attribute query here does it up front.
 namespace dkm {
+DKM_TU_FLAGS(cand, 0)
 __global__ void k_tu_cand() {}
 int preload_cand() {
   hipFuncAttributes a;

@@ -3280,15 +3280,13 @@ int dkm_add_f64_dd(double *hi, double *lo, const double *x, int64_t n,
   return check_launch("dkm_add_f64_dd");
 }
 
-// Result-invalidating A/B timing probes (variants.sh builds only): the
-// library reports them, and tests/test_isa_guard.py requires 0 of the
-// in-tree product build.
+// Result-invalidating A/B timing probes and A/B variant objects
+// (variants.sh / variants_b2.sh builds only): the library reports them,
+// and tests/test_isa_guard.py requires 0 of the in-tree product build.
 int dkm_build_flags(void) {
-#if DKM_AB_B1_PROBE || defined(DKM_DBG_NOCOMPUTE) || defined(DKM_DBG_NOLOAD)
-  return DKM_BUILD_TIMING_ONLY;
-#else
-  return b2_probe() ? DKM_BUILD_TIMING_ONLY : 0;
-#endif
+  return tu_flags_util() | tu_flags_dense() | tu_flags_b2() |
+         tu_flags_sorted() | tu_flags_cand() | tu_flags_sparse() |
+         tu_flags_gemm() | tu_flags_sums() | tu_flags_neighbors();
 }
 
 }  // extern "C"
@@ -3296,6 +3294,12 @@ int dkm_build_flags(void) {
 // Code-object preload (dkm_preload): the runtime loads this file's kernels
 // on first use of any of them; an attribute query here does it up front.
 namespace dkm {
+#if DKM_AB_B1_PROBE || defined(DKM_DBG_NOCOMPUTE) || defined(DKM_DBG_NOLOAD)
+#define DKM_DENSE_PROBE 1
+#else
+#define DKM_DENSE_PROBE 0
+#endif
+DKM_TU_FLAGS(dense, DKM_DENSE_PROBE)
 __global__ void k_tu_dense() {}
 int preload_dense() {
   hipFuncAttributes a;

@@ -1245,6 +1245,7 @@ template int gemm_image<float>(const float *, int64_t, int, int64_t,
 // Code-object preload (dkm_preload): the runtime loads this file's kernels
 // on first use of any of them; an attribute query here does it up front.
 namespace dkm {
+DKM_TU_FLAGS(gemm, 0)
 __global__ void k_tu_gemm() {}
 int preload_gemm() {
   hipFuncAttributes a;

@@ -30,6 +30,28 @@ int preload_gemm();
 int preload_sums();
 int preload_neighbors();
 int check_launch(const char *what);
+// Build flags per translation unit (dkm_build_flags ORs them):
+// DKM_BUILD_AB_VARIANT when the file was compiled as an A/B variant
+// (variants.sh / variants_b2.sh define DKM_AB_VARIANT=1 on every object
+// they compile with knobs), DKM_BUILD_TIMING_ONLY when one of the file's
+// result-invalidating probe knobs is set.
+#ifndef DKM_AB_VARIANT
+#define DKM_AB_VARIANT 0
+#endif
+#define DKM_TU_FLAGS(name, probe)                                  \
+  int tu_flags_##name() {                                          \
+    return (DKM_AB_VARIANT ? DKM_BUILD_AB_VARIANT : 0) |           \
+           ((probe) ? DKM_BUILD_TIMING_ONLY : 0);                  \
+  }
+int tu_flags_util();
+int tu_flags_dense();
+int tu_flags_b2();
+int tu_flags_sorted();
+int tu_flags_cand();
+int tu_flags_sparse();
+int tu_flags_gemm();
+int tu_flags_sums();
+int tu_flags_neighbors();
 
 // ---------------------------------------------------------------------------
 // Workspace layout (caller-allocated device memory, carved here).
@@ -56,7 +78,7 @@ struct WsHeader {
   int32_t pad3;
   uint64_t sfall_total;
 };
-constexpr uint64_t WS_MAGIC = 0x444b4d5753303033ull;  // "DKMWS003"
+constexpr uint64_t WS_MAGIC = 0x444b4d5753303034ull;  // "DKMWS004"
 constexpr size_t WS_HDR = 256;
 static_assert(sizeof(WsHeader) <= WS_HDR, "the header fits WS_HDR");
 

@@ -1276,6 +1276,7 @@ int dkm_radius_fill_csr_f64(const int64_t *indptr, const int32_t *indices,
 // Code-object preload (dkm_preload): the runtime loads this file's kernels
 // on first use of any of them; an attribute query here does it up front.
 namespace dkm {
+DKM_TU_FLAGS(neighbors, 0)
 __global__ void k_tu_neighbors() {}
 int preload_neighbors() {
   hipFuncAttributes a;

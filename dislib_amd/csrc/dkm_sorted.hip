@@ -615,6 +615,7 @@ int launch_screen_sorted(int64_t n, int d, int k, const WsView &v,
 // Code-object preload (dkm_preload): the runtime loads this file's kernels
 // on first use of any of them; an attribute query here does it up front.
 namespace dkm {
+DKM_TU_FLAGS(sorted, DKM_AB_SORTED_BSCALE != 1 || DKM_AB_SORTED_DBG != 0)
 __global__ void k_tu_sorted() {}
 int preload_sorted() {
   hipFuncAttributes a;

@@ -52,10 +52,12 @@
 // Samples are processed in chunks so that the S slice states fit the
 // workspace tail (20 bytes per slice and sample).
 //
-// The bound.  With u = 2^-24 (fp32), w = 2^-53 (fp64) and b = 2^-9 (bf16,
-// round to nearest), n stored entries, A_j >= sum |x_v c_jv| and M_j = xx +
+// The bound.  With u = 2^-24 (fp32), w = 2^-53 (fp64) and b = 2^-8 (bf16:
+// round to nearest to an 8-bit significand, unit roundoff 2^-8), n stored
+// entries, A_j >= sum |x_v c_jv| and M_j = xx +
 // |c_j|^2 + 2 A_j + |s_j| >= the magnitude of every partial result:
-//   bf16 table vs exact        b (1 + 2^-14) A_j (c_jv rounded to bf16)
+//   bf16 table vs exact        2 b (1 + 2^-14) A_j (c_jv rounded to bf16,
+//                                                in the -2 x.c term)
 //   fp32 dot vs exact          (n + 2) u A_j     (x rounded, fma chain)
 //   sklearn's fp64 dot         n w A_j
 //   s_j rounding, |c|^2 -> fp32  u |s_j| + u |c_j|^2
@@ -292,12 +294,14 @@ __global__ void __launch_bounds__(CSR_BLOCK)
         // the bound of every centre of the sample (header comment): A >=
         // sum |x_v c_jv| by Cauchy-Schwarz, |c_j|^2 <= cmax^2, |s_j| <=
         // |c_j|^2 + 2A; doubled, + 2^-100 for underflow; NaN / inf: no
-        // decision.  The bf16 table: 2 x (2 x b A) = 2^-7 A (1 + 2^-14).
+        // decision.  The bf16 table: 2 x (2 x b A) = 2^-6 A (1 + 2^-14)
+        // with b = 2^-8 (the fp64 -> fp32 -> bf16 double rounding is in
+        // the 1 + 2^-14).
         const float xx_up = xx * (1.f + (nf + 4.f) * 0x1.0p-23f);
         const float A = sqrtf(xx_up) * cmax * (1.f + 0x1.0p-20f);
         const float c2 = cmax * cmax * (1.f + 0x1.0p-22f);
         const float M = xx_up + 2.f * c2 + 4.f * A;
-        const float B = (0x1.0p-7f * (1.f + 0x1.0p-14f) * A +
+        const float B = (0x1.0p-6f * (1.f + 0x1.0p-14f) * A +
                          0x1.0p-23f * (2.f * c2 + 2.f * A +
                                        2.f * (nf + 2.f) * A) +
                          (2.f * nf + 6.f) * 0x1.0p-52f * M + 0x1.0p-100f) *
@@ -631,6 +635,7 @@ int dkm_predict_csr_f64(const int64_t *indptr, const int32_t *indices,
 // Code-object preload (dkm_preload): the runtime loads this file's kernels
 // on first use of any of them; an attribute query here does it up front.
 namespace dkm {
+DKM_TU_FLAGS(sparse, 0)
 __global__ void k_tu_sparse() {}
 int preload_sparse() {
   hipFuncAttributes a;

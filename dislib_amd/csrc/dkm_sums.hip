@@ -429,6 +429,7 @@ template int sorted_sums<double>(const double *, int64_t, int64_t, int,
 // Code-object preload (dkm_preload): the runtime loads this file's kernels
 // on first use of any of them; an attribute query here does it up front.
 namespace dkm {
+DKM_TU_FLAGS(sums, 0)
 __global__ void k_tu_sums() {}
 int preload_sums() {
   hipFuncAttributes a;

@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ C,
   const double *row = C + c * d;
   const int64_t ld = ct_ld(k);
   // the CSR screen's sliced bf16 C^T: slice c / w, column c % w; round to
-  // nearest (fp64 -> fp32 -> bf16: within 2^-9 (1 + 2^-14) relative, the
+  // nearest (fp64 -> fp32 -> bf16: within 2^-8 (1 + 2^-14) relative, the
   // bound's term)
   const int64_t w = csr_slice_width(k, d);
   uint16_t *ctbs = v.ctb + (c / w) * d * w + (c % w);
@@ -470,6 +470,8 @@ __global__ void __launch_bounds__(256) k_blobs(double *__restrict__ X,
     if (blob && t == 0) blob[i] = (int32_t)b;
   }
 }
+
+DKM_TU_FLAGS(util, 0)
 
 }  // namespace dkm
 

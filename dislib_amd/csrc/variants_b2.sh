@@ -11,7 +11,7 @@ objs=""
 for f in $srcs; do
   x=""; [ $f = dkm_sorted ] && x="-mllvm -amdgpu-atomic-optimizer-strategy=None"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off \
-    -fno-slp-vectorize $x $defs -c $f.hip -o v_${name}_$f.o
+    -fno-slp-vectorize $x -DDKM_AB_VARIANT=1 $defs -c $f.hip -o v_${name}_$f.o
   objs="$objs v_${name}_$f.o"
 done
 keep=$(for o in dkm_*.o; do b=${o%.o}; case " $srcs " in *" $b "*) ;; *) echo $o;; esac; done)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define DKM_ABI_VERSION 2
+#define DKM_ABI_VERSION 3
 
 /* error codes (besides hipError_t values passed through) */
 #define DKM_OK 0
@@ -348,12 +348,15 @@ int dkm_screen_counters(const void *ws, int64_t *out, void *stream);
 int dkm_screen_lists(const void *ws, size_t ws_bytes, int64_t *out,
                      void *stream);
 
-/* Build flags of this library: 0 for a product build.  Non-zero
- * (DKM_BUILD_TIMING_ONLY) when it was compiled with an A/B timing probe
- * that invalidates results (DKM_AB_B1_PROBE, DKM_DBG_NOCOMPUTE, ...): such a
- * library refuses every assignment call.  tests/test_isa_guard.py checks
+/* Build flags of this library: 0 for a product build.  DKM_BUILD_TIMING_ONLY
+ * when an object was compiled with an A/B timing probe that invalidates
+ * results (DKM_AB_B1_PROBE, DKM_AB_B2_PROBE, DKM_AB_SORTED_BSCALE != 1,
+ * DKM_AB_SORTED_DBG, DKM_DBG_NOCOMPUTE, ...); DKM_BUILD_AB_VARIANT when any
+ * object comes from an A/B variant build (csrc/variants*.sh).  bench.py
+ * records a non-zero value in its line, and tests/test_isa_guard.py checks
  * that the in-tree library reports 0. */
 #define DKM_BUILD_TIMING_ONLY 1
+#define DKM_BUILD_AB_VARIANT 2
 int dkm_build_flags(void);
 
 /* ------------------------------------------------------------------------

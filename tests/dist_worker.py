@@ -12,7 +12,7 @@ cuda:r and the per-iteration all-reduce goes through libdkm's own RCCL
 communicator (dkm_allreduce_*); the rank records its (nranks, rank) as
 that communicator reports them.
 
-  python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1
       --master-port P tests/dist_worker.py --case NAME --out PREFIX
       [--backend nccl]
 """
@@ -36,7 +36,28 @@ CASES = {
     "b2": (24000, 64, 200, 200, 2000, 6, 0.0, 0, 3),
     # CSR Subsets (the sparse screen + exact resolve), 10 entries per row
     "csr": (2000, 300, 0, 8, 250, 4, 0.0, 2, 2),
+    # world 4 (LAYOUT: Subset sizes instead of `subset`): ragged Subsets;
+    # 3 Subsets over 4 ranks (rank 0 -- whose REFRESH and initial centres
+    # win -- owns no rows and still joins every all-reduce); the
+    # single-product screen with the per-rank label-sorted image
+    "ragged4": (7001, 24, 9, 9, 0, 6, 0.0, 5, 2),
+    "empty4": (9500, 16, 12, 12, 0, 8, 0.0, 1, 3),
+    "sorted4": (24000, 64, 200, 200, 0, 8, 0.0, 0, 3),
 }
+LAYOUT = {
+    "ragged4": [700, 1300, 50, 2100, 900, 1, 1600, 350],
+    "empty4": [3000, 2500, 4000],
+    "sorted4": [5000, 7000, 3000, 9000],
+}
+
+
+def subsets(case):
+    """[(row0, row1)] of the case's Subsets."""
+    n, sub = CASES[case][0], CASES[case][4]
+    sizes = LAYOUT.get(case) or [min(sub, n - i) for i in range(0, n, sub)]
+    assert sum(sizes) == n
+    edges = np.concatenate([[0], np.cumsum(sizes)])
+    return [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:])]
 
 
 def data(case):
@@ -74,7 +95,7 @@ def main():
     import dislib_amd.cluster.kmeans as km_mod
     from dislib_amd import shard_dataset
     from dislib_amd.cluster import KMeans
-    from dislib_amd.data import load_data
+    from dislib_amd.data import Dataset, Subset
     n, d, blobs, k, sub, iters, tol, rs, refresh = CASES[a.case]
     km_mod.REFRESH = refresh if rank == 0 else 1000   # rank 0's value wins
     init = {}
@@ -86,15 +107,21 @@ def main():
         return c
     km_mod._init_centers = rec
     x = data(a.case)
-    ds = shard_dataset(load_data(x, sub))
+    full = Dataset(n_features=d, sparse=a.case == "csr")
+    for lo, hi in subsets(a.case):
+        full.append(Subset(x[lo:hi]))
+    ds = shard_dataset(full)
     km = KMeans(n_clusters=k, max_iter=iters, tol=tol, random_state=rs)
     km.fit_predict(ds)
     cen = km.centers.toarray() if hasattr(km.centers, "toarray") else \
         km.centers
     from dislib_amd import _shard
     info = _shard.comm_info(dev) if a.backend == "nccl" else None
+    lab = ds.labels_int32()
     np.savez("%s.%d.npz" % (a.out, rank), centers=cen,
-             n_iter=km.n_iter, labels=ds.labels_int32(), init=init["c"],
+             n_iter=km.n_iter, init=init["c"], nrows=np.array(
+                 sum(s.samples.shape[0] for s in ds)),
+             labels=lab if lab is not None else np.zeros(0, np.int32),
              refresh=np.array(km_mod.REFRESH),
              comm=np.array(info if info else (0, -1)))
     dist.barrier()

@@ -1,9 +1,10 @@
-"""Multi-process (world_size 2, gloo, CPU) tests of the N>1 path's host
+"""Multi-process (world_size 2 and 4, gloo, CPU) tests of the N>1 path's host
 logic: Subset sharding, the packed [sums | counts] all-reduce that replaces
 the reference's `_merge` arity tree (cluster/kmeans/base.py:137-143), the
 init-centre broadcast, and replicated convergence decisions.  The per-rank
 partial sums come from the oracle (the GPU kernels are covered by the -m gpu
 parity tests)."""
+import functools
 import os
 import socket
 
@@ -87,6 +88,52 @@ def _lloyd_emulation(rank, world):
             return C, it
 
 
+def _lloyd_sizes(rank, world, sizes):
+    """The distributed Lloyd loop of _lloyd_emulation over Subsets of the
+    given sizes (ragged; fewer Subsets than ranks leaves ranks empty):
+    (centres, n_iter, rows owned, labels of the last assignment)."""
+    from sklearn.datasets import make_blobs
+    from dislib_amd import _shard
+    from dislib_amd.data import Dataset, Subset
+    from oracle import kmeans_oracle as orc
+    x, _ = make_blobs(n_samples=sum(sizes), n_features=5, centers=4,
+                      random_state=7)
+    ds = Dataset(n_features=5)
+    edges = np.concatenate([[0], np.cumsum(sizes)])
+    for a, b in zip(edges[:-1], edges[1:]):
+        ds.append(Subset(x[a:b]))
+    mine = _shard.shard_dataset(ds, rank, world)
+    k, d = 4, 5
+    C = orc.init_centers(d, False, k, 7)
+    _shard.broadcast_(torch.from_numpy(C))
+    it = 0
+    while True:
+        acc = np.zeros(k * (d + 1))
+        labs = []
+        for s in mine:
+            lab, sums, cnt = orc.partial_sum(s.samples, C)
+            labs.append(lab)
+            acc[:k * d] += sums.ravel()
+            acc[k * d:] += cnt
+        t = torch.from_numpy(acc)
+        _shard.allreduce_sum_(t)      # every rank joins, empty or not
+        acc = t.numpy()
+        old = C.copy()
+        cnt = acc[k * d:]
+        sums = acc[:k * d].reshape(k, d)
+        for c in range(k):
+            if cnt[c] != 0:
+                C[c] = sums[c] / cnt[c]
+        it += 1
+        diff = sum(np.linalg.norm(C[c] - old[c]) for c in range(k))
+        conv = int(diff < 1e-4 ** 2 or it >= 10)
+        assert _shard.agree(conv)
+        if conv:
+            rows = sum(s.samples.shape[0] for s in mine)
+            return C, it, rows, (np.concatenate(labs) if labs else
+                                 np.zeros(0, np.int64))
+
+
 def _allreduce_matches_global(rank, world):
     from dislib_amd import _shard
     from dislib_amd.data import load_data
@@ -152,3 +199,33 @@ def _shard_under_world(rank, world):
 def test_shard_dataset_under_world():
     res = _run(_shard_under_world)
     assert res[0] == ((0, 2), 3) and res[1] == ((1, 2), 4)
+
+
+@pytest.mark.parametrize("sizes", [
+    [700, 1300, 50, 2100, 900, 1, 1600, 350],     # ragged, 2 per rank
+    [3000, 2500, 4000],                           # rank 0 owns nothing
+    [10, 20],                                     # two empty ranks
+])
+def test_world4_ragged_and_empty_shards(sizes):
+    """World size 4: ragged Subsets and ranks without rows (which still join
+    every all-reduce) give the single-process result: identical centres
+    and n_iter on every rank, every row labelled once, the oracle's fit."""
+    from sklearn.datasets import make_blobs
+    from oracle import kmeans_oracle as orc
+    res = _run(functools.partial(_lloyd_sizes, sizes=sizes), world=4)
+    c0, i0, _, _ = res[0]
+    for r in range(4):
+        assert np.array_equal(res[r][0], c0) and res[r][1] == i0
+    assert sum(res[r][2] for r in range(4)) == sum(sizes)
+    if len(sizes) < 4:
+        assert res[0][2] == 0
+    x, _ = make_blobs(n_samples=sum(sizes), n_features=5, centers=4,
+                      random_state=7)
+    edges = np.concatenate([[0], np.cumsum(sizes)])
+    ref = orc.OracleKMeans(n_clusters=4, random_state=7)
+    rl = ref.fit([x[a:b] for a, b in zip(edges[:-1], edges[1:])],
+                 set_labels=True)
+    assert i0 == ref.n_iter
+    np.testing.assert_allclose(c0, ref.centers, rtol=1e-12, atol=1e-12)
+    lab = np.concatenate([res[r][3] for r in range(4)])
+    assert np.array_equal(lab, rl)

@@ -291,6 +291,51 @@ def test_csr_predict_and_partial_sum_vs_oracle(n, d, k, per_row, seed, nq):
     assert np.array_equal(got[k * d:], want[:, d])
 
 
+@pytest.mark.parametrize("seed,scale", [(0, 1.0), (1, 1e3), (2, 1e-3)])
+def test_csr_near_ties_at_the_bf16_table_rounding(seed, scale):
+    """CSR samples whose two nearest centres differ below the bf16 C^T
+    rounding (dkm_sparse.hip bound: 2^-8 relative per table entry, the
+    screen's 2 B covers 2^-6 A): pairs of centres c, c (1 + r 2^-8) on a
+    shared 12-column support (r = 0: exact ties, first index), samples on
+    10 of those columns near c.  The distance gaps span about
+    +-2^-7 |x||c|, where the bf16 screen alone can order them wrongly;
+    labels must equal the oracle's sklearn-order arithmetic."""
+    from dislib_amd import _device, _lib
+    rng = np.random.default_rng(seed)
+    n, d, pairs = 4000, 2000, 32
+    k = 2 * pairs
+    C = np.zeros((k, d))
+    sup = [np.sort(rng.choice(d, 12, replace=False)) for _ in range(pairs)]
+    for m, s in enumerate(sup):
+        C[2 * m, s] = rng.uniform(0.5, 1.0, 12) * scale
+        r = rng.uniform(-1, 1, 12) * (m % 8 != 0)        # some exact ties
+        C[2 * m + 1, s] = C[2 * m, s] * (1 + r * 2.0 ** -8)
+    rows, cols, vals = [], [], []
+    for i in range(n):
+        m = rng.integers(pairs)
+        c = np.sort(rng.choice(sup[m], 10, replace=False))
+        rows += [i] * 10
+        cols += list(c)
+        vals += list(C[2 * m, c] * (1 + rng.normal(0, 0.003, 10)))
+    xs = sp.csr_matrix((vals, (rows, cols)), shape=(n, d))
+    xs.sort_indices()
+    rl, _, _ = orc.partial_sum(xs, sp.csr_matrix(C), sparse=True)
+    assert len(np.unique(rl % 2)) == 2          # both members of pairs win
+    dev = torch.device("cuda")
+    ds = _load(xs, n)
+    dd = ds._device_data()
+    Ct = torch.from_numpy(C).to(dev)
+    ws = _device.Workspace(k, d, dd.n, dev)
+    acc = torch.empty(k * (d + 1), dtype=torch.float64, device=dev)
+    lab = torch.empty(dd.n, dtype=torch.int32, device=dev)
+    _device.prepare(Ct, ws, acc, csr=True)
+    _device.partial_sum(dd, Ct, ws, lab, acc, _lib.MODE_AUTO)
+    assert np.array_equal(lab.cpu().numpy(), rl)
+    lab2 = torch.full((dd.n,), -7, dtype=torch.int32, device=dev)
+    _device.predict(dd, Ct, ws, lab2, _lib.MODE_AUTO)
+    assert np.array_equal(lab2.cpu().numpy(), rl)
+
+
 # ---------------------------------------------------------------------------
 # kernel-level parity against the oracle on seeded inputs
 # ---------------------------------------------------------------------------
