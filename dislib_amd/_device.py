@@ -74,6 +74,7 @@ class DeviceData:
     def __init__(self, dataset, device=None):
         self.device = resolve(device)
         self.images = {}            # sample images by kind (screen_image)
+        self._unbuilt = set()       # kinds allocated, not yet built
         self._image_failed = set()
         subsets = list(dataset)
         self.sizes = [int(s.samples.shape[0]) for s in subsets]
@@ -139,11 +140,14 @@ class DeviceData:
     # -- the sample image ---------------------------------------------------
     def screen_image(self, k, mode):
         """The resident bf16 operand image of X (dkm_x_image_*) when the
-        screen that (k, d, mode) selects reads one, as (tensor, kind);
-        built on first use (stream-ordered, one pass over X) and kept with
-        the data, which is immutable (one image per kind).  (None, 0) when
-        not useful, disabled (DKM_X_IMAGE=0) or when it would leave less
-        than 4 GiB of HBM free."""
+        screen that (k, d, mode) selects reads one, as (tensor, kind); kept
+        with the data, which is immutable (one image per kind).  On first
+        use it is only allocated and returned as kind | IMAGE_BUILD: the
+        assignment call that receives it builds it (the d <= 32 screen's
+        full-sums pass writes it while it converts X anyway) and
+        :meth:`image_built` records that.  (None, 0) when not useful,
+        disabled (DKM_X_IMAGE=0) or when it would leave less than 4 GiB of
+        HBM free."""
         if self.sparse or not X_IMAGE or self.n == 0:
             return None, 0
         so = _lib.lib()
@@ -151,7 +155,8 @@ class DeviceData:
         if kind == 0:
             return None, 0
         if self.images.get(kind) is not None:
-            return self.images[kind], kind
+            return self.images[kind], kind | (
+                _lib.IMAGE_BUILD if kind in self._unbuilt else 0)
         if kind in self._image_failed:
             return None, 0
         t = torch()
@@ -162,17 +167,19 @@ class DeviceData:
             return None, 0
         img = _alloc("image%d" % kind, nb, lambda: t.empty(
             nb, dtype=t.uint8, device=self.device))
-        fn = so.dkm_x_image_f32 if self.dtype == np.float32 else \
-            so.dkm_x_image_f64
-        _lib.check(fn(ptr(self.X), self.n, self.d, self.X.stride(0), kind,
-                      ptr(img), nb, stream_ptr()), "dkm_x_image")
         self.images[kind] = img
-        return img, kind
+        self._unbuilt.add(kind)
+        return img, kind | _lib.IMAGE_BUILD
+
+    def image_built(self, kind):
+        """The call that received kind | IMAGE_BUILD returned: built."""
+        self._unbuilt.discard(kind & ~_lib.IMAGE_BUILD)
 
     def drop_images(self):
         """Free the resident sample images (up to 16.5 GB at C3): later
         calls convert X in the screen, or build an image again."""
         self.images = {}
+        self._unbuilt = set()
         self._image_failed = set()
 
     # -- helpers -----------------------------------------------------------
@@ -299,6 +306,7 @@ def partial_sum(dd, C, ws, labels, acc, mode, image=None):
         _lib.check(fn(ptr(dd.X), ptr(img), kind, img.numel(), dd.n, dd.d,
                       dd.X.stride(0), ptr(C), k, ws.p, ws.nbytes, ptr(labels),
                       ptr(acc), mode, stream_ptr()), "dkm_partial_sum_img")
+        dd.image_built(kind)
         return
     fn = so.dkm_partial_sum_f32 if dd.dtype == np.float32 else \
         so.dkm_partial_sum_f64
@@ -324,6 +332,7 @@ def assign_delta(dd, C, ws, labels, delta, mode, image=None):
         _lib.check(fn(ptr(dd.X), ptr(img), kind, img.numel(), dd.n, dd.d,
                       dd.X.stride(0), ptr(C), k, ws.p, ws.nbytes, ptr(labels),
                       ptr(delta), mode, stream_ptr()), "dkm_assign_delta_img")
+        dd.image_built(kind)
         return
     fn = so.dkm_assign_delta_f32 if dd.dtype == np.float32 else \
         so.dkm_assign_delta_f64

@@ -15,6 +15,7 @@ ABI_VERSION = 3
 MODE_AUTO, MODE_EXACT, MODE_SCREEN32, MODE_BF16X3, MODE_BF16 = 0, 1, 2, 3, 4
 MODE_MASK, MODE_NOHINT, MODE_B1 = 0xff, 0x100, 0x200
 IMAGE_NONE, IMAGE_SINGLE, IMAGE_SPLIT, IMAGE_SORTED, IMAGE_GEMM = 0, 1, 2, 3, 4
+IMAGE_BUILD = 0x100   # kind flag: build the allocated image during the call
 SUMS_F64, SUMS_F32, SUMS_RECIP = 0, 1, 2
 PREP_CSR = 1
 COMM_ID_BYTES = 128

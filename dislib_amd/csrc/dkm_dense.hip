@@ -566,6 +566,17 @@ __device__ __forceinline__ bool resolve_lane(
 // sample loop is block-uniform (waves past n compute on zero rows and write
 // nothing) so that every wave reaches the chunk barriers.  L2 -> LDS traffic
 // per block step = all fragments (k * dpad * 4 B) per 16 * NB * SB/64 rows.
+//
+// T3 (CHUNK bf16x3: C3's iteration 0 against the U[0, 1) initial centres):
+// each lane keeps a packed top-3 (one more v_med3 per score) and the running
+// top-3 carries the first two centres' indices, so the decision is
+// three-way like the single-product screens': s2 - s1 > 2B -> the label;
+// else s3 - s1 > 2B -> the two candidates go to the wave's candidate list
+// (k_cand2 applies the reference arithmetic to both; use_list bit 2, labels-
+// only launches with d % 8 == 0); else the re-check list.  Against U[0, 1)
+// centres ~2 % of the rows are near-ties under the bf16x3 bound, nearly all
+// with two candidates (tools/exp note in DESIGN.md 3.13): they no longer
+// cost a fp32 re-scan of all k centres each.
 template <int PREC, int NKS, int NB, bool VEC, class TX, bool CHUNK>
 __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
     k_screen(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
@@ -608,9 +619,16 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
   const int64_t step = (int64_t)gridDim.x * (SB / 64) * 16 * NB;
   const int64_t seg = (int64_t)blockIdx.x * (SB / 64) + wid;
   int2 *wl = v.tlist + seg * TL_CAP;  // this wave's undecided samples
-  const bool listing = use_list && seg < TL_SEGS;
+  const bool listing = (use_list & 1) && seg < TL_SEGS;
   int tl_cnt = 0;   // wave-uniform: listed samples
   int tl_over = 0;  // wave-uniform: undecided samples left for the re-check
+  constexpr bool T3 = CHUNK && PREC == P_B3;
+  // two-candidate list (T3, labels-only launches): (offset, c1 | c2 << 16)
+  const bool list2 = T3 && (use_list & 2) && v.clist && seg < B1_SEGS;
+  int2 *cl = list2 ? v.clist + seg * B1_CAP : nullptr;
+  int cl_cnt = 0;
+  const float pinf = __uint_as_float(opaque_u32(0x7f800000u));
+  (void)pinf;
 
   double tile[NB][NKS][8];
   // delta: the previous labels of the tile's samples travel with the tile
@@ -744,13 +762,16 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
 #endif
 
     // running (value, centre index) top-2 of this lane over all groups
-    float r1[NB], r2[NB];
-    int ri[NB];
+    // (T3: top-3, the second's index in ri2)
+    float r1[NB], r2[NB], r3[NB];
+    int ri[NB], ri2[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       r1[b] = INFINITY;
       r2[b] = INFINITY;
+      r3[b] = INFINITY;
       ri[b] = 0;
+      ri2[b] = 0;
     }
     // MFMA chain of centre block cb into accv[], started from |c|^2; consumed
     // one chain later so that the next block's MFMAs overlap this block's
@@ -806,11 +827,12 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
     cbase = c0;
     for (int g0 = c0; g0 < c1; g0 += GROUP_BLOCKS) {
       const int g1 = min(c1, g0 + GROUP_BLOCKS);
-      float b1[NB], b2[NB];  // packed, this group
+      float b1[NB], b2[NB], b3[NB];  // packed, this group
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
         b1[b] = INFINITY;
         b2[b] = INFINITY;
+        b3[b] = INFINITY;
       }
       auto score = [&](int cb, const f32x4 (&accv)[NB]) {
         const uint32_t ib = (uint32_t)((cb - g0) * 4);  // wave-uniform tag
@@ -826,7 +848,9 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
             // note on packed-VALU operand hazards; built -fno-slp-vectorize)
             const float sp = __uint_as_float(
                 (__float_as_uint(accv[b][i]) & vmask) | tag[i]);
-            // b1 <= b2: new second = med3(b1, b2, s)
+            // b1 <= b2 (<= b3): new third = med3(b2, b3, s), new second =
+            // med3(b1, b2, s)
+            if constexpr (T3) b3[b] = __builtin_amdgcn_fmed3f(b2[b], b3[b], sp);
             b2[b] = __builtin_amdgcn_fmed3f(b1[b], b2[b], sp);
             b1[b] = min_nc(b1[b], sp, ninf);
           }
@@ -848,7 +872,24 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
         const uint32_t tg = __float_as_uint(b1[b]) & PACK_MASK;
         const int gi = (g0 + (int)(tg >> 2)) * 16 + 4 * q + (int)(tg & 3);
         const bool nw = b1[b] < r1[b];
-        r2[b] = nw ? min_nc(r1[b], b2[b], ninf) : min_nc(r2[b], b1[b], ninf);
+        if constexpr (T3) {
+          // merge sorted (r1, r2, r3) with (b1, b2, b3): the third smallest
+          // of the union is min(r3, b3, max(r1, b2), max(r2, b1)); ties keep
+          // the running entry (earlier groups: lower indices)
+          const uint32_t t2 = __float_as_uint(b2[b]) & PACK_MASK;
+          const int gi2 = (g0 + (int)(t2 >> 2)) * 16 + 4 * q + (int)(t2 & 3);
+          r3[b] = min_nc(min_nc(r3[b], b3[b], ninf),
+                         min_nc(__builtin_amdgcn_fmed3f(r1[b], b2[b], pinf),
+                                __builtin_amdgcn_fmed3f(r2[b], b1[b], pinf),
+                                ninf),
+                         ninf);
+          const bool s2 = nw ? (b2[b] < r1[b]) : (b1[b] < r2[b]);
+          const float v2 = nw ? (s2 ? b2[b] : r1[b]) : (s2 ? b1[b] : r2[b]);
+          ri2[b] = nw ? (s2 ? gi2 : ri[b]) : (s2 ? gi : ri2[b]);
+          r2[b] = v2;
+        } else {
+          r2[b] = nw ? min_nc(r1[b], b2[b], ninf) : min_nc(r2[b], b1[b], ninf);
+        }
         ri[b] = nw ? gi : ri[b];
         r1[b] = nw ? b1[b] : r1[b];
       }
@@ -865,10 +906,42 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
       vi = tc ? ci : ai;
       v2 = tc ? min_nc(a1, c2, ninf) : min_nc(a2, c1, ninf);
     };
+    // T3: merge two (value, index) top-3 lists with the first two indices
+    // (symmetric in the pair: both lanes hold the same result)
+    auto merge3 = [&](int b, float a1, float a2, float a3, int ai, int ai2,
+                      float c1, float c2, float c3, int ci, int ci2) {
+      const bool tc = (c1 < a1) | ((c1 == a1) & (ci < ai));
+      const float x = tc ? a1 : c1, y = tc ? c2 : a2;
+      const int xi = tc ? ai : ci, yi = tc ? ci2 : ai2;
+      const bool ty = (y < x) | ((y == x) & (yi < xi));
+      r3[b] = min_nc(min_nc(a3, c3, ninf),
+                     min_nc(__builtin_amdgcn_fmed3f(a1, c2, pinf),
+                            __builtin_amdgcn_fmed3f(a2, c1, pinf), ninf),
+                     ninf);
+      r1[b] = tc ? c1 : a1;
+      ri[b] = tc ? ci : ai;
+      r2[b] = ty ? y : x;
+      ri2[b] = ty ? yi : xi;
+    };
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       float a1, c1, a2, c2;
       int ai, ci;
+      if constexpr (T3) {
+        float a3, c3;
+        int aj, cj;
+#define DKM_T3_ROUND(OFF)                                          \
+  pair_xor<OFF>(r1[b], a1, c1);                                    \
+  pair_xor<OFF>(r2[b], a2, c2);                                    \
+  pair_xor<OFF>(r3[b], a3, c3);                                    \
+  pair_xor<OFF>(ri[b], ai, ci);                                    \
+  pair_xor<OFF>(ri2[b], aj, cj);                                   \
+  merge3(b, a1, a2, a3, ai, aj, c1, c2, c3, ci, cj);
+        DKM_T3_ROUND(16)
+        DKM_T3_ROUND(32)
+#undef DKM_T3_ROUND
+        continue;
+      }
       pair_xor<16>(r1[b], a1, c1);
       pair_xor<16>(r2[b], a2, c2);
       pair_xor<16>(ri[b], ai, ci);
@@ -885,8 +958,23 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
       const float B2 = bound2_fast(bk, xx[b], xn);
       const bool sane = (xn < 1e18f) & (xn * cm < 1e30f) & (r1[b] < 1e30f);
       const bool unique = sane & (r2[b] - r1[b] > B2);
-      const bool und = si < n && !unique;
       const int prev = delta ? prv[b] : -1;
+      // T3: exactly two candidates -> the candidate list (k_cand2)
+      bool two = false;
+      if constexpr (T3) {
+        two = list2 && si < n && sane && !unique && (r3[b] - r1[b] > B2);
+        const uint64_t mc = __ballot(q == 0 && two);
+        const int addc = __popcll(mc);
+        if (cl_cnt + addc <= B1_CAP) {
+          if (q == 0 && two)
+            cl[cl_cnt + lane_prefix(mc)] =
+                make_int2((int)(si - base), ri[b] | (ri2[b] << 16));
+          cl_cnt += addc;
+        } else {
+          two = false;   // list full: the re-check list takes it
+        }
+      }
+      const bool und = si < n && !unique && !two;
       // undecided samples join the wave's list (resolved in the tail) while
       // it has room; the rest are counted for the re-check pass
       const uint64_t um = __ballot(q == 0 && und);
@@ -938,6 +1026,7 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
   }
   if (lane == 0) {
     if (listing) v.tcount[seg] = tl_cnt;
+    if (list2) v.ccount[seg] = cl_cnt;
     if (tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
   }
   if (amode & AM_INLDS) {
@@ -979,7 +1068,8 @@ __global__ void __launch_bounds__(SBW) __attribute__((
     amdgpu_waves_per_eu(DKM_W32_WPE)))
     k_screen_w32(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
                  int k, WsView v, int32_t *__restrict__ lab_out, double *acc,
-                 int amode, int64_t base, int use_list, XImage img) {
+                 int amode, int64_t base, int use_list, XImage img,
+                 int build) {
   constexpr int GB = 8;  // 32-centre blocks per packing group
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int nkb = (int)(kpad32(k) / 32);
@@ -1168,6 +1258,18 @@ __global__ void __launch_bounds__(SBW) __attribute__((
     wave_sync_w();
     xx = s_xx[r];
     prv = pv;
+    if (build) {
+      // DKM_IMAGE_BUILD: this tile of the split image (k_x_image_split's
+      // layout: hi slices 0, 1 then lo 0, 1, lane l = row l & 31, features
+      // 16 (l >> 5) + 8 s ..) and the screen's own fp32 |x|^2 -- the image
+      // launches of later iterations then score exactly these operands
+      bf16x8 *dst = (bf16x8 *)(img.tiles + (s0 >> 5) * 2048) + lane;
+      dst[0] = xh[0];
+      dst[64] = xh[1];
+      dst[128] = xl[0];
+      dst[192] = xl[1];
+      if (h == 0) ((float *)img.xx)[s0 + r] = xx;
+    }
     if (!full_acc && s_next < n) load_tile(s_next);
     }  // !IMG
 
@@ -2365,10 +2467,11 @@ static int launch_screen_w32(const TX *X, int64_t end, int d, int64_t ldx,
                              int k, const WsView &v, int32_t *lab_out,
                              double *acc, int amode, int64_t base, size_t lds,
                              int use_list, hipStream_t s, int *nseg,
-                             XImage img) {
-  // the image serves launches that need no sums from the raw rows
-  const bool im = img.tiles && img.kind == IMG_SPLIT && !am_full(amode) &&
-                  base % 32 == 0;
+                             XImage img, bool build = false) {
+  // the image serves launches that need no sums from the raw rows; a build
+  // launch (full sums, base 0) writes it instead
+  const bool im = !build && img.tiles && img.kind == IMG_SPLIT &&
+                  !am_full(amode) && base % 32 == 0;
   const void *kf = im ? (const void *)k_screen_w32<TX, true>
                       : (const void *)k_screen_w32<TX, false>;
   lds += (size_t)(SBW / 64) * W32_SCR;  // the waves' transpose scratch
@@ -2379,11 +2482,12 @@ static int launch_screen_w32(const TX *X, int64_t end, int d, int64_t ldx,
   *nseg = (int)std::min<int64_t>((int64_t)g * (SBW / 64), TL_SEGS);
   if (im)
     k_screen_w32<TX, true><<<g, SBW, lds, s>>>(X, end, d, ldx, k, v, lab_out,
-                                               acc, amode, base, use_list, img);
+                                               acc, amode, base, use_list, img,
+                                               0);
   else
     k_screen_w32<TX, false><<<g, SBW, lds, s>>>(
         X, end, d, ldx, k, v, lab_out, acc, amode, base, use_list,
-        XImage{nullptr, nullptr, IMG_NONE});
+        build ? img : XImage{nullptr, nullptr, IMG_NONE}, build ? 1 : 0);
   return check_launch("screen assignment (32x32)");
 }
 
@@ -2723,7 +2827,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                          int64_t ldx, const double *C, int k, const WsView &v,
                          size_t wsb, int32_t *labels, double *acc,
                          int acc_kind, hipStream_t s, XImage img,
-                         bool nohint = false, bool force_b1 = false) {
+                         bool nohint = false, bool force_b1 = false,
+                         void *build_img = nullptr) {
   (void)wsb;
   const int64_t nq = std::min<int64_t>(v.nq, INT32_MAX);
   if (!labels && nq < 1)
@@ -2777,6 +2882,21 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const int amode = acc_mode(skind, lds_fits);
   const size_t lds = fb + ((amode & AM_INLDS) ? a_bytes : 0);
   const int use_list = list_ok(k, d) && !AB_NO_LIST ? 1 : 0;
+  // the chunked bf16x3 screen's two-candidate list (T3 in k_screen): labels-
+  // only launches whose rows k_cand2 can take (d % 8 == 0, d <= 128)
+  const bool c2 = !b1 && !w32 && chb && prec == P_B3 && amode == AM_NONE &&
+                  v.clist && vec && d % 8 == 0 && d >= 8 && d <= 128;
+  // DKM_IMAGE_BUILD: the split image written by this call's full-sums w32
+  // pass over X (one launch from row 0), else built first
+  bool fuse_build = false;
+  if (build_img) {
+    fuse_build = w32 && am_full(amode) && img.kind == IMG_SPLIT && chunk >= n;
+    if (!fuse_build) {
+      if (int r = launch_x_image<TX>(X, n, d, ldx, img.kind, build_img,
+                                     dev_info().cus, s))
+        return r;
+    }
+  }
   for (int64_t base = 0; base < n; base += chunk) {
     const int64_t end = std::min(n, base + chunk);
     int32_t *lab_out = labels ? labels : v.queue - base;
@@ -2800,7 +2920,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                                            nseg, s);
     } else if (w32)
       r = launch_screen_w32<TX>(X, end, d, ldx, k, v, lab_out, acc, amode,
-                                base, lds, use_list, s, &nseg, img);
+                                base, lds, use_list, s, &nseg, img,
+                                fuse_build);
     else if (prec == P_F32)
       r = vec ? launch_screen_nks<P_F32, true, TX>(X, end, d, ldx, k, v,
                                                    lab_out, acc, amode, base,
@@ -2811,11 +2932,15 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
     else
       r = vec ? launch_screen_nks<P_B3, true, TX>(X, end, d, ldx, k, v,
                                                   lab_out, acc, amode, base,
-                                                  lds, use_list, chb, s, &nseg)
+                                                  lds, use_list | (c2 ? 2 : 0),
+                                                  chb, s, &nseg)
               : launch_screen_nks<P_B3, false, TX>(X, end, d, ldx, k, v,
                                                    lab_out, acc, amode, base,
                                                    lds, use_list, chb, s, &nseg);
     if (r) return r;
+    if (c2 && (r = launch_cand2<TX>(X, d, ldx, C, v, lab_out, base,
+                                    std::min(nseg, B1_SEGS), s)))
+      return r;
     if ((use_list || b1) && (r = launch_list<TX>(X, d, ldx, k, v, lab_out,
                                                   acc, skind, vec, base,
                                                   nseg, s)))
@@ -2881,6 +3006,11 @@ static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
 }
 
 template <class TX>
+static int x_image(const TX *X, int64_t n, int64_t d, int64_t ldx, int kind,
+                   void *image, size_t image_bytes, void *stream,
+                   const char *who);
+
+template <class TX>
 static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                   const double *C, int64_t k, const void *ws, size_t wsb,
                   int32_t *labels, double *acc, int acc_kind, int mode,
@@ -2897,6 +3027,13 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
   hipStream_t s = (hipStream_t)stream;
   if (mode & ~(DKM_MODE_MASK | DKM_MODE_NOHINT | DKM_MODE_B1))
     return fail(DKM_E_ARG, std::string(who) + ": unknown mode flags");
+  // DKM_IMAGE_BUILD: build the (allocated, unbuilt) image during this call
+  const bool build = image && (image_kind & DKM_IMAGE_BUILD);
+  image_kind &= ~DKM_IMAGE_BUILD;
+  if (build && image_kind == IMG_SORTED)
+    return fail(DKM_E_ARG, std::string(who) +
+                               ": the sorted image is built by "
+                               "dkm_x_image_sorted_*");
   const bool nohint = mode & DKM_MODE_NOHINT, force_b1 = mode & DKM_MODE_B1;
   mode &= DKM_MODE_MASK;
   if (mode == DKM_MODE_AUTO)
@@ -2919,6 +3056,14 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
     return fail(DKM_E_ARG, std::string(who) +
                                ": the sorted image needs the single-product "
                                "screen (MODE_SCREEN_BF16 or AUTO) and labels");
+  const bool split_w32 = image_kind == IMG_SPLIT && mode ==
+      DKM_MODE_SCREEN_BF16X3 && screen_ok(k, d) && d <= 32;
+  if (build && !split_w32) {
+    // no screen writes this kind in its pass: build it first
+    if (int r = x_image<TX>(X, n, d, ldx, image_kind, (void *)image,
+                            x_image_bytes(n, d, image_kind), stream, who))
+      return r;
+  }
   if (mode == DKM_MODE_EXACT)
     return launch_exact<TX>(X, n, (int)d, ldx, C, (int)k, labels, acc,
                             acc_kind, s);
@@ -2949,7 +3094,8 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                              : XImage{nullptr, nullptr, IMG_NONE, nullptr,
                                       nullptr};
     return launch_screen<TX>(prec, X, n, (int)d, ldx, C, (int)k, v, wsb,
-                             labels, acc, acc_kind, s, img, nohint, force_b1);
+                             labels, acc, acc_kind, s, img, nohint, force_b1,
+                             build && split_w32 ? (void *)image : nullptr);
   }
   return fail(DKM_E_ARG, std::string(who) + ": bad mode");
 }
@@ -3177,7 +3323,8 @@ int dkm_x_image_sorted_sums_f32(const float *X, int64_t n, int64_t d,
 }
 
 #define DKM_IMG_CHECK(who)                                                  \
-  if (image && image_bytes < dkm_x_image_bytes(n, d, image_kind))           \
+  if (image && image_bytes < dkm_x_image_bytes(                             \
+                                 n, d, image_kind & ~DKM_IMAGE_BUILD))      \
     return fail(DKM_E_ARG, std::string(who) +                               \
                                ": image_bytes does not match n, d and kind");
 

@@ -148,12 +148,18 @@ int dkm_assign_delta_f32(const float *X, int64_t n, int64_t d, int64_t ldx,
  * dkm_x_image_kind(k, d, mode) says which kind the selected screen reads
  * (DKM_IMAGE_NONE: building one would be wasted).  The _img forms of
  * dkm_partial_sum / dkm_assign_delta take it (image NULL = none); every
- * other argument is theirs.  Same interface as base.py:166-181.          */
+ * other argument is theirs.  Same interface as base.py:166-181.
+ * image_kind | DKM_IMAGE_BUILD: the image memory is allocated but not built
+ * yet; the call builds it (the d <= 32 bf16x3 screen's full-sums pass writes
+ * the split image while it converts X anyway -- no separate pass over X --
+ * any other call builds it first with dkm_x_image_*), after which the
+ * caller passes the kind without the flag.                                */
 #define DKM_IMAGE_NONE 0
 #define DKM_IMAGE_SINGLE 1
 #define DKM_IMAGE_SPLIT 2
 #define DKM_IMAGE_SORTED 3
 #define DKM_IMAGE_GEMM 4
+#define DKM_IMAGE_BUILD 0x100
 int dkm_x_image_kind(int64_t k, int64_t d, int mode);
 size_t dkm_x_image_bytes(int64_t n, int64_t d, int kind);
 int dkm_x_image_f64(const double *X, int64_t n, int64_t d, int64_t ldx,

@@ -106,3 +106,65 @@ def test_image_kind_per_config():
     assert so.dkm_x_image_kind(1000, 64, _lib.MODE_AUTO) == _lib.IMAGE_SINGLE
     assert so.dkm_x_image_kind(4096, 1024, _lib.MODE_AUTO) == _lib.IMAGE_GEMM
     assert so.dkm_x_image_kind(4096, 1024, _lib.MODE_EXACT) == _lib.IMAGE_NONE
+
+
+@pytest.mark.parametrize("n,d,k,f32", [(40011, 32, 100, False),
+                                       (9000, 20, 64, False),
+                                       (5000, 16, 10, True),
+                                       (777, 8, 300, False)])
+def test_full_sums_pass_builds_the_split_image(n, d, k, f32):
+    """DKM_IMAGE_BUILD: the d <= 32 screen's full-sums pass (a fit's
+    iteration 0) writes the split image while it converts X: the hi / lo
+    tiles equal dkm_x_image_*'s bit for bit, |x|^2 is the screen's own fp32
+    sum (within 2^-22 of the exact one), and the call's labels and sums are
+    the oracle's; a delta launch through the fused image then matches the
+    oracle too."""
+    from dislib_amd import _device, _lib
+    from dislib_amd.data import load_data
+    so = _lib.lib()
+    rng = np.random.default_rng(n + d + k)
+    blobs = rng.uniform(-10, 10, (k, d))
+    x = blobs[rng.integers(0, k, n)] + rng.standard_normal((n, d))
+    if f32:
+        x = x.astype(np.float32)
+    C = blobs + 0.3 * rng.standard_normal((k, d))
+    dev = torch.device("cuda", 0)
+    dd = load_data(x, subset_size=n)._device_data()
+    ws = _device.Workspace(k, d, n, dev)
+    acc = torch.zeros(k * (d + 1), dtype=torch.float64, device=dev)
+    Ct = torch.from_numpy(C).to(dev)
+    lab = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    mode = _lib.MODE_BF16X3
+    _device.prepare(Ct, ws, acc)
+    img, kind = dd.screen_image(k, mode)
+    assert kind == _lib.IMAGE_SPLIT | _lib.IMAGE_BUILD
+    img.fill_(0xAB)                       # garbage: the call must write all
+    _device.partial_sum(dd, Ct, ws, lab, acc, mode)
+    assert not dd._unbuilt
+    rl, rs, rc = orc.partial_sum(x, C)
+    assert np.array_equal(lab.cpu().numpy(), rl)
+    a = acc.cpu().numpy()
+    assert np.array_equal(a[k * d:], rc.astype(np.float64))
+    err = np.max(np.abs(a[:k * d].reshape(k, d) - rs) /
+                 np.maximum(np.abs(rs), 1.0))
+    assert err <= (1e-4 if f32 else 1e-11)
+    # against the separate builder
+    nb = so.dkm_x_image_bytes(n, d, _lib.IMAGE_SPLIT)
+    ref = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    fn = so.dkm_x_image_f32 if f32 else so.dkm_x_image_f64
+    _lib.check(fn(_device.ptr(dd.X), n, d, d, _lib.IMAGE_SPLIT,
+                  _device.ptr(ref), nb, _device.stream_ptr()), "image")
+    nt = (n + 31) // 32
+    got, want = img.cpu().numpy(), ref.cpu().numpy()
+    assert np.array_equal(got[:nt * 4096], want[:nt * 4096])
+    gx = got[nt * 4096:nt * 4096 + 4 * n].view(np.float32)
+    wx = want[nt * 4096:nt * 4096 + 4 * n].view(np.float32)
+    assert np.all(np.abs(gx - wx) <= 2.0 ** -22 * wx)
+    # a delta launch through the fused image
+    C2 = C + 0.2 * rng.standard_normal(C.shape)
+    Ct2 = torch.from_numpy(C2).to(dev)
+    acc.zero_()
+    _device.prepare(Ct2, ws, acc)
+    _device.assign_delta(dd, Ct2, ws, lab, acc, mode)
+    rl2, _, _ = orc.partial_sum(x, C2)
+    assert np.array_equal(lab.cpu().numpy(), rl2)

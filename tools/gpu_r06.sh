@@ -53,6 +53,7 @@ trace() {  # name limit cmd...
 for s in "$@"; do
   case $s in
     t_new) step t_new 900 $PT tests/test_gpu_dist.py tests/test_gpu_parity.py::test_csr_near_ties_at_the_bf16_table_rounding ;;
+    t_core) step t_core 900 $PT tests/test_gpu_image.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py::test_c2_full_size_labels tests/test_gpu_fullsize.py::test_c3_full_size_labels ;;
     t_sorted) step t_sorted 900 $PT tests/test_gpu_sorted.py tests/test_gpu_b2.py tests/test_gpu_fullsize.py::test_c3_full_size_labels ;;
     t_all) step t_all 1100 $PT -m gpu tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
