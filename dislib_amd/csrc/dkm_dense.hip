@@ -2112,6 +2112,82 @@ __device__ __forceinline__ void recheck_finish_count(
     atomicAdd((unsigned long long *)&v.hdr->rechecked_total, *blk_count);
 }
 
+// resolve_lane's two stages for ONE sample i with the whole wave: lanes
+// over centres (jc = lane, lane + 64, ...), the same fp32 scores and bound
+// (stage 1), then the reference arithmetic on the centres within the bound
+// (stage 2; every centre when the scores are not sane), reduced over the
+// wave by (distance, index).  The re-check list's stage-2 samples go here:
+// lane per sample, a sample with many candidates (a near-tie among many
+// centres) held its whole wave for k sequential exact distances.
+template <int MAXD, class TX>
+__device__ __forceinline__ void resolve_wave(
+    const TX *__restrict__ X, int64_t ldx, int d, int k, int64_t i, int prev,
+    const float *cl, const float *cnl, int dp, float cm, const double *ct64,
+    int32_t *lab_out, int amode, const AccTarget &at) {
+  const int lane = threadIdx.x & 63;
+  const TX *xr = X + i * ldx;
+  float xf[MAXD];
+  float xx = 0.f;
+#pragma unroll
+  for (int t = 0; t < MAXD; ++t) {      // the same fp32 chain as resolve_lane
+    xf[t] = t < d ? (float)ld_x(xr + t) : 0.f;
+    xx = fmaf(xf[t], xf[t], xx);
+  }
+  auto score = [&](int jc) {
+    const float *cr = cl + (int64_t)jc * dp;
+    float dot = 0.f;
+#pragma unroll
+    for (int t = 0; t < MAXD; ++t)
+      if (t < dp) dot = fmaf(xf[t], cr[t], dot);
+    return fmaf(-2.f, dot, cnl[jc]);
+  };
+  float b1 = INFINITY, b2 = INFINITY;
+  int i1 = INT32_MAX;
+  for (int jc = lane; jc < k; jc += 64) {
+    const float sc = score(jc);
+    i1 = sc < b1 ? jc : i1;
+    b2 = __builtin_amdgcn_fmed3f(b1, b2, sc);
+    b1 = fminf(b1, sc);
+  }
+  // wave top-2 (NaN scores never win: fminf / med3 drop them, and the sane
+  // test below sends such a sample to stage 2 over every centre)
+  for (int off = 1; off < 64; off <<= 1) {
+    const float o1 = __shfl_xor(b1, off, 64), o2 = __shfl_xor(b2, off, 64);
+    const int oi = __shfl_xor(i1, off, 64);
+    const bool tk = (o1 < b1) | ((o1 == b1) & (oi < i1));
+    b2 = tk ? fminf(b1, o2) : fminf(b2, o1);
+    i1 = tk ? oi : i1;
+    b1 = tk ? o1 : b1;
+  }
+  const float xn = sqrtf(xx) * (1.0f + (d + 4) * 0x1.0p-24f);
+  const float B = screen_bound<P_F32>(d, xn, cm, false);
+  const bool sane = (xn < 1e18f) && (xn * cm < 1e30f) && (b1 < 1e30f);
+  int bi = i1;
+  if (!(sane && b2 - b1 > 2.0f * B)) {
+    const float lim = b1 + 2.0f * B;
+    double best = INFINITY;
+    bi = INT32_MAX;
+    for (int jc = lane; jc < k; jc += 64) {
+      if (sane && !(score(jc) <= lim)) continue;
+      const SqDiffT<TX> f{xr, ct64 + jc, ct_ld(k)};
+      const double dist = argmin_key(sqrt(pw_leaf(f, 0, d)));
+      if (dist < best || bi == INT32_MAX) {
+        best = dist;
+        bi = jc;
+      }
+    }
+    for (int off = 1; off < 64; off <<= 1) {
+      const double ob = __shfl_xor(best, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      const bool tk = (ob < best) | ((ob == best) & (oi < bi));
+      best = tk ? ob : best;
+      bi = tk ? oi : bi;
+    }
+  }
+  if (lane == 0) lab_out[i] = bi;
+  recheck_accumulate(amode, at, xr, d, bi, prev, lane);
+}
+
 constexpr int RL_CAP = 128;  // per-wave list: a full batch + one chunk
 
 static size_t recheck_lane_lds(int64_t, int64_t) {
@@ -2231,10 +2307,13 @@ __global__ void __launch_bounds__(BLOCK)
   unsigned long long mine = 0;
   int2 *dl = dlist[threadIdx.x >> 6];
   int dcnt = 0;  // wave-uniform
-  auto stage2 = [&](int2 it) {
-    resolve_lane<MAXD, VEC, TX>(X, ldx, d, k, base + it.x, it.y, v.c32,
-                                v.cn32, dp,
-                                cm, v.ct64, lab_out, amode, at);
+  // stage 2: one listed sample at a time over the whole wave
+  auto stage2 = [&](int cnt) {
+    for (int r = 0; r < cnt; ++r) {
+      const int2 it = dl[r];
+      resolve_wave<MAXD, TX>(X, ldx, d, k, base + it.x, it.y, v.c32, v.cn32,
+                             dp, cm, v.ct64, lab_out, amode, at);
+    }
   };
 #if DKM_LIST_SPREAD
   // (segment, 64-sample batch) pairs dealt round-robin over all waves, batch
@@ -2269,7 +2348,7 @@ __global__ void __launch_bounds__(BLOCK)
       dcnt += __popcll(m);
       if (dcnt >= 64) {
         wave_lds_sync();
-        stage2(dl[lane]);
+        stage2(64);
         const int rem = dcnt - 64;
         const int2 tail = lane < rem ? dl[64 + lane] : make_int2(0, 0);
         wave_lds_sync();
@@ -2279,7 +2358,7 @@ __global__ void __launch_bounds__(BLOCK)
     }
   }
   wave_lds_sync();
-  if (lane < dcnt) stage2(dl[lane]);
+  stage2(dcnt);
   recheck_finish_count(mine, &blk_count, v);
   if (amode & AM_INLDS) flush_lds_acc(lds_acc, acc, k, d);
 }
