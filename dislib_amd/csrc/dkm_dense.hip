@@ -577,7 +577,8 @@ __device__ __forceinline__ bool resolve_lane(
 // centres ~2 % of the rows are near-ties under the bf16x3 bound, nearly all
 // with two candidates (tools/exp note in DESIGN.md 3.13): they no longer
 // cost a fp32 re-scan of all k centres each.
-template <int PREC, int NKS, int NB, bool VEC, class TX, bool CHUNK>
+template <int PREC, int NKS, int NB, bool VEC, class TX, bool CHUNK,
+          bool T3P = false>
 __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
     k_screen(const TX *__restrict__ X, int64_t n, int d, int64_t ldx, int k,
              WsView v, int32_t *__restrict__ lab_out, double *acc, int amode,
@@ -622,7 +623,7 @@ __global__ void __launch_bounds__(SB) DKM_SCREEN_WPE(NKS, CHUNK)
   const bool listing = (use_list & 1) && seg < TL_SEGS;
   int tl_cnt = 0;   // wave-uniform: listed samples
   int tl_over = 0;  // wave-uniform: undecided samples left for the re-check
-  constexpr bool T3 = CHUNK && PREC == P_B3;
+  constexpr bool T3 = T3P && CHUNK && PREC == P_B3;
   // two-candidate list (T3, labels-only launches): (offset, c1 | c2 << 16)
   const bool list2 = T3 && (use_list & 2) && v.clist && seg < B1_SEGS;
   int2 *cl = list2 ? v.clist + seg * B1_CAP : nullptr;
@@ -2307,14 +2308,16 @@ __global__ void __launch_bounds__(BLOCK)
   unsigned long long mine = 0;
   int2 *dl = dlist[threadIdx.x >> 6];
   int dcnt = 0;  // wave-uniform
-  // stage 2: one listed sample at a time over the whole wave
-  auto stage2 = [&](int cnt) {
-    for (int r = 0; r < cnt; ++r) {
-      const int2 it = dl[r];
-      resolve_wave<MAXD, TX>(X, ldx, d, k, base + it.x, it.y, v.c32, v.cn32,
-                             dp, cm, v.ct64, lab_out, amode, at);
-    }
+  auto stage2 = [&](int2 it) {
+    resolve_lane<MAXD, VEC, TX>(X, ldx, d, k, base + it.x, it.y, v.c32,
+                                v.cn32, dp,
+                                cm, v.ct64, lab_out, amode, at);
   };
+  // stage-2 samples go to the global list that k_recheck_wave resolves a
+  // wave per sample (v.smoved as (offset, prev) pairs; the per-wave LDS
+  // list only takes what overflows it)
+  int2 *s2l = (int2 *)v.smoved;
+  const uint32_t s2cap = (uint32_t)std::min<int64_t>(v.nq / 2, INT32_MAX);
 #if DKM_LIST_SPREAD
   // (segment, 64-sample batch) pairs dealt round-robin over all waves, batch
   // index major: every resident wave gets work and the segments' row loads
@@ -2343,12 +2346,21 @@ __global__ void __launch_bounds__(BLOCK)
                                                v.ct64,
                                                lab_out, amode, at);
       }
-      const unsigned long long m = __ballot(!ok);
+      unsigned long long m = __ballot(!ok);
+      if (m) {
+        uint32_t pos = 0;
+        if (lane == 0) pos = atomicAdd(&v.hdr->s2count, (uint32_t)__popcll(m));
+        pos = (uint32_t)__shfl((int)pos, 0, 64);
+        const uint32_t p = pos + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+        if (!ok && p < s2cap) s2l[p] = it;
+        m = __ballot(!ok && p >= s2cap);   // the rest: this wave, stage 2
+        ok = ok || p < s2cap;
+      }
       if (!ok) dl[dcnt + __popcll(m & ((1ull << lane) - 1))] = it;
       dcnt += __popcll(m);
       if (dcnt >= 64) {
         wave_lds_sync();
-        stage2(64);
+        stage2(dl[lane]);
         const int rem = dcnt - 64;
         const int2 tail = lane < rem ? dl[64 + lane] : make_int2(0, 0);
         wave_lds_sync();
@@ -2358,9 +2370,37 @@ __global__ void __launch_bounds__(BLOCK)
     }
   }
   wave_lds_sync();
-  stage2(dcnt);
+  if (lane < dcnt) stage2(dl[lane]);
   recheck_finish_count(mine, &blk_count, v);
   if (amode & AM_INLDS) flush_lds_acc(lds_acc, acc, k, d);
+}
+
+// k_recheck_list's stage-2 samples (fp32 stage 1 could not decide them),
+// one wave per sample: lanes over centres (resolve_wave), so a sample with
+// many candidates no longer holds a lane -- and its wave -- for a walk over
+// every centre with one exact distance after another (the 1-4 ms spikes of
+// the steady C3 iterations).  Sums by global fp64 atomics (rare samples).
+template <int MAXD, class TX>
+__global__ void __launch_bounds__(BLOCK)
+    k_recheck_wave(const TX *__restrict__ X, int d, int64_t ldx, int k,
+                   WsView v, int32_t *__restrict__ lab_out, double *acc,
+                   int amode, int64_t base) {
+  const uint32_t cap = (uint32_t)std::min<int64_t>(v.nq / 2, INT32_MAX);
+  const uint32_t cnt = min(v.hdr->s2count, cap);
+  const int64_t wv = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+  const int64_t nwv = (int64_t)gridDim.x * (BLOCK / 64);
+  if (wv >= cnt) return;
+  const int dp = (int)round_up(d, 4);
+  const float cm =
+      (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
+  const int am = amode & ~AM_INLDS;
+  const AccTarget at = acc_target(am, nullptr, acc, k, d);
+  const int2 *s2l = (const int2 *)v.smoved;
+  for (int64_t r = wv; r < cnt; r += nwv) {
+    const int2 it = s2l[r];
+    resolve_wave<MAXD, TX>(X, ldx, d, k, base + it.x, it.y, v.c32, v.cn32,
+                           dp, cm, v.ct64, lab_out, am, at);
+  }
 }
 
 template <bool SMALL, class TX>
@@ -2525,18 +2565,19 @@ static int screen_chunk_blocks(int64_t k, int64_t d) {
   return (int)std::max<int64_t>(1, (int64_t)LDS_BUDGET / per);
 }
 
-template <int PREC, int NKS, int NB, bool VEC, class TX, bool CHUNK>
+template <int PREC, int NKS, int NB, bool VEC, class TX, bool CHUNK,
+          bool T3P = false>
 static int launch_screen_t(const TX *X, int64_t end, int d, int64_t ldx,
                            int k, const WsView &v, int32_t *lab_out,
                            double *acc, int amode, int64_t base, size_t lds,
                            int use_list, int chb, hipStream_t s, int *nseg) {
-  const void *kf = (const void *)k_screen<PREC, NKS, NB, VEC, TX, CHUNK>;
+  const void *kf = (const void *)k_screen<PREC, NKS, NB, VEC, TX, CHUNK, T3P>;
   const int64_t cap = (int64_t)dev_info().cus * resident_blocks(kf, SB, lds);
   const int64_t per_block = 16 * NB * (SB / 64);
   const int64_t need = (end - base + per_block - 1) / per_block;
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min(need, cap));
   *nseg = (int)std::min<int64_t>((int64_t)g * (SB / 64), TL_SEGS);
-  k_screen<PREC, NKS, NB, VEC, TX, CHUNK><<<g, SB, lds, s>>>(
+  k_screen<PREC, NKS, NB, VEC, TX, CHUNK, T3P><<<g, SB, lds, s>>>(
       X, end, d, ldx, k, v, lab_out, acc, amode, base, use_list, chb);
   return check_launch("screen assignment");
 }
@@ -2578,9 +2619,15 @@ static int launch_screen_nks(const TX *X, int64_t end, int d, int64_t ldx,
                              int *nseg) {
 #define DKM_SCREEN_CASE(NKS, NB)                                             \
   case NKS:                                                                  \
-    return chb ? launch_screen_t<PREC, NKS, DKM_NB_CHUNK, VEC, TX, true>(    \
-                     X, end, d, ldx, k, v, lab_out, acc, amode, base, lds,   \
-                     use_list, chb, s, nseg)                                 \
+    return chb ? ((use_list & 2)                                             \
+                      ? launch_screen_t<PREC, NKS, DKM_NB_CHUNK, VEC, TX,    \
+                                        true, true>(                         \
+                            X, end, d, ldx, k, v, lab_out, acc, amode, base, \
+                            lds, use_list, chb, s, nseg)                     \
+                      : launch_screen_t<PREC, NKS, DKM_NB_CHUNK, VEC, TX,    \
+                                        true>(                               \
+                            X, end, d, ldx, k, v, lab_out, acc, amode, base, \
+                            lds, use_list, chb, s, nseg))                    \
                : launch_screen_t<PREC, NKS, NB, VEC, TX, false>(             \
                      X, end, d, ldx, k, v, lab_out, acc, amode, base, lds,   \
                      use_list, chb, s, nseg);
@@ -2669,9 +2716,14 @@ static int launch_list_t(const TX *X, int d, int64_t ldx, int k,
   const int64_t g = std::max<int64_t>(
       1, std::min<int64_t>((int64_t)dev_info().cus * per_cu,
                            (units + BLOCK / 64 - 1) / (BLOCK / 64)));
+  if (hipMemsetAsync(&v.hdr->s2count, 0, 4, s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "list re-check: counter reset");
   k_recheck_list<MAXD, VEC, TX><<<(unsigned)g, BLOCK, lds, s>>>(
       X, d, ldx, k, v, lab_out, acc, amode, base, nseg);
-  return check_launch("list re-check");
+  if (int r = check_launch("list re-check")) return r;
+  k_recheck_wave<MAXD, TX><<<(unsigned)(dev_info().cus * 4), BLOCK, 0, s>>>(
+      X, d, ldx, k, v, lab_out, acc, amode, base);
+  return check_launch("list re-check (stage 2, wave per sample)");
 }
 
 // Can the listed samples be resolved lane-per-sample (k_recheck_list)?
@@ -2899,6 +2951,136 @@ static int launch_candn(const TX *X, int d, int64_t ldx, const double *C,
   return check_launch("N-candidate re-check");
 }
 
+// ---- the re-screen of a screen's re-check list ---------------------------
+// Per-segment offsets of the list (exclusive prefix of tcount) and its total
+// (one block, nseg <= TL_SEGS).
+__global__ void __launch_bounds__(1024)
+    k_list_scan(const int32_t *__restrict__ tcount, int nseg,
+                int32_t *__restrict__ prefix, uint32_t *total) {
+  __shared__ int32_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (nseg + 1023) / 1024;
+  const int a = min(nseg, t * per), b = min(nseg, a + per);
+  int sum = 0;
+  for (int i = a; i < b; ++i) sum += min(max(tcount[i], 0), TL_CAP);
+  part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  for (int i = a; i < b; ++i) {
+    prefix[i] = run;
+    run += min(max(tcount[i], 0), TL_CAP);
+  }
+  if (t == 1023) *total = (uint32_t)part[1023];
+}
+
+// The list compacted: a wave per segment.
+__global__ void __launch_bounds__(256)
+    k_list_compact(const int2 *__restrict__ tlist,
+                   const int32_t *__restrict__ tcount,
+                   const int32_t *__restrict__ prefix, int nseg,
+                   int2 *__restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t sg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); sg < nseg;
+       sg += (int64_t)gridDim.x * 4) {
+    const int cnt = min(max(tcount[sg], 0), TL_CAP);
+    const int2 *src = tlist + sg * TL_CAP;
+    int2 *dst = out + prefix[sg];
+    for (int i = lane; i < cnt; i += 64) dst[i] = src[i];
+  }
+}
+
+// rows base + list[r].x of X -> out (m x d, packed)
+template <class TX>
+__global__ void __launch_bounds__(256)
+    k_gather_rows(const TX *__restrict__ X, int64_t ldx, int d,
+                  const int2 *__restrict__ list, int m, int64_t base,
+                  TX *__restrict__ out) {
+  const int64_t tot = (int64_t)m * d;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t r = e / d;
+    const int t = (int)(e - r * d);
+    out[e] = X[(base + list[r].x) * ldx + t];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+    k_scatter_labels(const int32_t *__restrict__ lab,
+                     const int2 *__restrict__ list, int m,
+                     int32_t *__restrict__ lab_out) {
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < m;
+       r += (int64_t)gridDim.x * 256)
+    lab_out[list[r].x] = lab[r];
+}
+
+template <class TX>
+static int launch_screen(int prec, const TX *X, int64_t n, int d,
+                         int64_t ldx, const double *C, int k, const WsView &v,
+                         size_t wsb, int32_t *labels, double *acc,
+                         int acc_kind, hipStream_t s, XImage img,
+                         bool nohint = false, bool force_b1 = false,
+                         void *build_img = nullptr, bool sub = false);
+
+// The samples a screen left to the exact re-check (its per-wave lists) are
+// gathered, RS_ROWS at a time, and screened again by the chunked bf16x3
+// screen with the two-candidate list (k_screen T3 + k_cand2), the list's
+// leftovers by its own re-check; their labels are scattered back.  A single-
+// product screen's list (~2^-8 bound) mostly resolves to one or two
+// candidates under bf16x3 (~2^-16), so those samples skip the re-check's
+// fp32 scan of all k centres (lane per sample, latency-bound: 6-7 ms for
+// C3 iteration 1's 1.15M listed rows, 1-4 ms spikes for a few hundred rows
+// in steady iterations); the bf16x3 screen's own list (C3 iteration 0,
+// ~2 % of the rows against the initial centres) gains the two-candidate
+// path, at the top-3 cost on those rows only.  One 4-byte device -> host
+// read per call (the list's length sizes the gathered chunks).
+template <class TX>
+static int rescreen_list(const TX *X, int d, int64_t ldx, const double *C,
+                         int k, const WsView &v, size_t wsb, int32_t *lab_out,
+                         int64_t base, int nseg, hipStream_t s) {
+  nseg = std::min(nseg, TL_SEGS);
+  if (nseg <= 0) return 0;
+  k_list_scan<<<1, 1024, 0, s>>>(v.tcount, nseg, v.rprefix, &v.hdr->rtotal);
+  if (int r = check_launch("re-screen: list scan")) return r;
+  uint32_t tot = 0;
+  if (hipMemcpyAsync(&tot, &v.hdr->rtotal, 4, hipMemcpyDeviceToHost, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "re-screen: list length");
+  if (tot == 0) return 0;
+  const int cus = dev_info().cus;
+  k_list_compact<<<(unsigned)std::min<int64_t>((nseg + 3) / 4, cus * 8), 256,
+                   0, s>>>(v.tlist, v.tcount, v.rprefix, nseg, v.rlist);
+  if (int r = check_launch("re-screen: compact")) return r;
+  for (int64_t c0 = 0; c0 < (int64_t)tot; c0 += RS_ROWS) {
+    const int m = (int)std::min<int64_t>(RS_ROWS, (int64_t)tot - c0);
+    const unsigned g = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>(((int64_t)m * d + 255) / 256, (int64_t)cus * 16));
+    k_gather_rows<TX><<<g, 256, 0, s>>>(X, ldx, d, v.rlist + c0, m, base,
+                                        (TX *)v.rx);
+    if (int r = check_launch("re-screen: gather")) return r;
+    if (int r = launch_screen<TX>(P_B3, (const TX *)v.rx, m, d, d, C, k, v,
+                                  wsb, v.rlab, nullptr, 0, s,
+                                  XImage{nullptr, nullptr, IMG_NONE, nullptr,
+                                         nullptr},
+                                  false, false, nullptr, true))
+      return r;
+    k_scatter_labels<<<(unsigned)std::max(1, std::min((m + 255) / 256,
+                                                      cus * 8)),
+                       256, 0, s>>>(v.rlab, v.rlist + c0, m, lab_out + base);
+    if (int r = check_launch("re-screen: scatter")) return r;
+  }
+  // the screen's lists are done: the caller's list pass finds nothing
+  if (hipMemsetAsync(v.tcount, 0, (size_t)TL_SEGS * 4, s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "re-screen: list reset");
+  return 0;
+}
+
 // Screen + exact re-check over [0, n).  Labels go to `labels` when given,
 // else to the workspace scratch (queue region), in chunks of its capacity.
 template <class TX>
@@ -2906,8 +3088,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                          int64_t ldx, const double *C, int k, const WsView &v,
                          size_t wsb, int32_t *labels, double *acc,
                          int acc_kind, hipStream_t s, XImage img,
-                         bool nohint = false, bool force_b1 = false,
-                         void *build_img = nullptr) {
+                         bool nohint, bool force_b1, void *build_img,
+                         bool sub) {
   (void)wsb;
   const int64_t nq = std::min<int64_t>(v.nq, INT32_MAX);
   if (!labels && nq < 1)
@@ -2963,8 +3145,17 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
   const int use_list = list_ok(k, d) && !AB_NO_LIST ? 1 : 0;
   // the chunked bf16x3 screen's two-candidate list (T3 in k_screen): labels-
   // only launches whose rows k_cand2 can take (d % 8 == 0, d <= 128)
-  const bool c2 = !b1 && !w32 && chb && prec == P_B3 && amode == AM_NONE &&
-                  v.clist && vec && d % 8 == 0 && d >= 8 && d <= 128;
+  // (sub: this call is a re-screen's, on gathered rows)
+  const bool c2 = sub && !b1 && !w32 && chb && prec == P_B3 &&
+                  amode == AM_NONE && v.clist && vec && d % 8 == 0 &&
+                  d >= 8 && d <= 128;
+  // the re-screen of this call's re-check list: labels-only screens whose
+  // gathered rows the chunked bf16x3 screen with its two-candidate list
+  // takes (c2's conditions on the gathered, packed rows)
+  const bool rescreen = !sub && v.rlist && amode == AM_NONE && use_list &&
+                        screen_chunk_blocks(k, d) > 0 &&
+                        (b1 || (prec == P_B3 && chb && !w32)) &&
+                        d % 8 == 0 && d >= 8 && d <= 128;
   // DKM_IMAGE_BUILD: the split image written by this call's full-sums w32
   // pass over X (one launch from row 0), else built first
   bool fuse_build = false;
@@ -3019,6 +3210,9 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
     if (r) return r;
     if (c2 && (r = launch_cand2<TX>(X, d, ldx, C, v, lab_out, base,
                                     std::min(nseg, B1_SEGS), s)))
+      return r;
+    if (rescreen && (r = rescreen_list<TX>(X, d, ldx, C, k, v, wsb, lab_out,
+                                           base, nseg, s)))
       return r;
     if ((use_list || b1) && (r = launch_list<TX>(X, d, ldx, k, v, lab_out,
                                                   acc, skind, vec, base,
@@ -3174,7 +3368,8 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                                       nullptr};
     return launch_screen<TX>(prec, X, n, (int)d, ldx, C, (int)k, v, wsb,
                              labels, acc, acc_kind, s, img, nohint, force_b1,
-                             build && split_w32 ? (void *)image : nullptr);
+                             build && split_w32 ? (void *)image : nullptr,
+                             false);
   }
   return fail(DKM_E_ARG, std::string(who) + ": bad mode");
 }

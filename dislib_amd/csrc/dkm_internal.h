@@ -61,12 +61,12 @@ struct WsHeader {
   int64_t k, d, dpad, n_queue;
   uint64_t cmax_bits;       // max_c ||c||_2 as ordered bits (non-negative)
   uint32_t qcount;          // samples queued for exact re-check this call
-  uint32_t pad0;
+  uint32_t s2count;         // k_recheck_list's stage-2 samples (global list)
   uint64_t rechecked_total; // diagnostics
   uint32_t gcount;          // GEMM screen: candidate-list entries (per chunk)
   uint32_t gcount2;         // GEMM screen: full-scan entries (per chunk)
   int32_t nmoved;           // sorted sums: samples whose label changed
-  uint32_t pad1;
+  uint32_t rtotal;          // re-screen: entries of the screen's re-check list
   uint32_t csr_nund;        // CSR screen: undecided samples of this chunk
   uint32_t pad2;
   uint64_t reserved[5];
@@ -125,6 +125,14 @@ inline size_t b1_frag_bytes(int64_t k, int64_t d) {
 inline bool b1_ok(int64_t k, int64_t d) {
   return d <= 128 && k >= 2 && k <= 32767 && b1_frag_bytes(k, d) <= B1_LDS_MAX;
 }
+// The re-screen (dkm_dense.hip rescreen_list): the samples a screen leaves
+// to the exact re-check are gathered and screened again by the chunked
+// bf16x3 screen with its two-candidate list.  Shapes of the single-product
+// screens with rows k_cand2 takes; RS_ROWS rows per gathered chunk.
+constexpr int64_t RS_ROWS = 262144;
+inline bool rescreen_ok(int64_t k, int64_t d) {
+  return b1_ok(k, d) && d % 8 == 0 && d >= 8;
+}
 
 // GEMM screen eligibility: the register-tile screen takes d <= 128
 inline bool gemm_path(int64_t k, int64_t d) {
@@ -162,6 +170,13 @@ struct WsView {
   int32_t *ncount; // b1_ok: entries used per screen wave
   int2 *tlist;    // TL_SEGS x TL_CAP undecided (offset, prev) per screen wave
   int32_t *tcount; // TL_SEGS entries used per screen wave
+  // re-screen of the re-check list (rescreen_ok shapes, else nullptr): the
+  // list compacted (TL_SEGS x TL_CAP entries), its per-segment offsets, and
+  // a chunk of RS_ROWS gathered rows (fp64 or fp32) with their labels
+  int2 *rlist;
+  int32_t *rprefix;
+  int32_t *rlab;
+  void *rx;
   // block skipping of k_screen_b2 (mind_ok(k, d), else NULL): k x MIND_LD
   // lower bounds of the distance from centre p to the nearest other centre
   // of each 32-centre block (+inf past the last block)

@@ -73,6 +73,12 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
     b += (size_t)B1_SEGS * B1_NCAP * 16;            // nlist
     b += (size_t)B1_SEGS * 4;                       // ncount
   }
+  if (rescreen_ok(k, d)) {
+    b += (size_t)TL_SEGS * TL_CAP * 8;              // rlist
+    b += (size_t)TL_SEGS * 4;                       // rprefix
+    b += (size_t)RS_ROWS * 4;                       // rlab
+    b += (size_t)RS_ROWS * d * 8;                   // rx
+  }
   if (k <= SORT_KMAX) b += round_up((k + 1) * 4, 256) + 2 * round_up(k * 4, 256);
   b += 3 * round_up(n_queue * 4, 256);  // queue, sitems, smoved
   return b;
@@ -158,6 +164,20 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
     p += (size_t)B1_SEGS * B1_NCAP * 16;
     v->ncount = (int32_t *)p;
     p += (size_t)B1_SEGS * 4;
+  }
+  v->rlist = nullptr;
+  v->rprefix = nullptr;
+  v->rlab = nullptr;
+  v->rx = nullptr;
+  if (rescreen_ok(k, d)) {
+    v->rlist = (int2 *)p;
+    p += (size_t)TL_SEGS * TL_CAP * 8;
+    v->rprefix = (int32_t *)p;
+    p += (size_t)TL_SEGS * 4;
+    v->rlab = (int32_t *)p;
+    p += (size_t)RS_ROWS * 4;
+    v->rx = (void *)p;
+    p += (size_t)RS_ROWS * d * 8;
   }
   v->soff = v->scur = v->scnt = nullptr;
   if (k <= SORT_KMAX) {
