@@ -2287,7 +2287,7 @@ template <int MAXD, bool VEC, class TX>
 __global__ void __launch_bounds__(BLOCK)
     k_recheck_list(const TX *__restrict__ X, int d, int64_t ldx, int k,
                    WsView v, int32_t *__restrict__ lab_out, double *acc,
-                   int amode, int64_t base, int nseg) {
+                   int amode, int64_t base, int nseg, int wave_all) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int dp = (int)round_up(d, 4);
   // (fp32 centres: global, scalar loads in resolve_lane)
@@ -2341,10 +2341,11 @@ __global__ void __launch_bounds__(BLOCK)
       bool ok = true;
       if (t0 + lane < cnt) {
         it = e[t0 + lane];
-        ok = resolve_lane<MAXD, VEC, TX, true>(X, ldx, d, k, base + it.x,
+        // wave_all (short lists): every sample straight to k_recheck_wave
+        ok = !wave_all &&
+             resolve_lane<MAXD, VEC, TX, true>(X, ldx, d, k, base + it.x,
                                                it.y, v.c32, v.cn32, dp, cm,
-                                               v.ct64,
-                                               lab_out, amode, at);
+                                               v.ct64, lab_out, amode, at);
       }
       unsigned long long m = __ballot(!ok);
       if (m) {
@@ -2709,7 +2710,7 @@ template <int MAXD, bool VEC, class TX>
 static int launch_list_t(const TX *X, int d, int64_t ldx, int k,
                          const WsView &v, int32_t *lab_out, double *acc,
                          int amode, int64_t base, int nseg, size_t lds,
-                         hipStream_t s) {
+                         hipStream_t s, bool wave_all) {
   const void *kf = (const void *)k_recheck_list<MAXD, VEC, TX>;
   const int per_cu = resident_blocks(kf, BLOCK, lds);
   const int64_t units = DKM_LIST_SPREAD ? (int64_t)nseg * (TL_CAP / 64) : nseg;
@@ -2719,7 +2720,7 @@ static int launch_list_t(const TX *X, int d, int64_t ldx, int k,
   if (hipMemsetAsync(&v.hdr->s2count, 0, 4, s) != hipSuccess)
     return fail(DKM_E_LAUNCH, "list re-check: counter reset");
   k_recheck_list<MAXD, VEC, TX><<<(unsigned)g, BLOCK, lds, s>>>(
-      X, d, ldx, k, v, lab_out, acc, amode, base, nseg);
+      X, d, ldx, k, v, lab_out, acc, amode, base, nseg, wave_all ? 1 : 0);
   if (int r = check_launch("list re-check")) return r;
   k_recheck_wave<MAXD, TX><<<(unsigned)(dev_info().cus * 4), BLOCK, 0, s>>>(
       X, d, ldx, k, v, lab_out, acc, amode, base);
@@ -2731,11 +2732,15 @@ static bool list_ok(int64_t k, int64_t d) {
   return d <= 128 && recheck_lane_lds(k, d) <= LDS_BUDGET;
 }
 
+// wave_all: the list is short (a re-screen's leftovers): every sample goes
+// to k_recheck_wave (a wave per sample, its latency spread over the chip)
+// instead of lane-per-sample stage 1, whose per-wave walk over all k centres
+// costs ~1 ms whatever the list's length.
 template <class TX>
 static int launch_list(const TX *X, int d, int64_t ldx, int k,
                        const WsView &v, int32_t *lab_out, double *acc,
                        int acc_kind, bool vec, int64_t base, int nseg,
-                       hipStream_t s) {
+                       hipStream_t s, bool wave_all = false) {
   const size_t fb = 0;  // centres are read from global (scalar loads)
   const size_t a_bytes = (size_t)lds_acc_len(k, d) * 8;
   const int amode = acc_mode(acc_kind, fb + a_bytes <= LDS_BUDGET);
@@ -2743,9 +2748,9 @@ static int launch_list(const TX *X, int d, int64_t ldx, int k,
   const int maxd = d <= 32 ? 32 : d <= 64 ? 64 : 128;
 #define DKM_LL(M)                                                            \
   (vec ? launch_list_t<M, true, TX>(X, d, ldx, k, v, lab_out, acc, amode,    \
-                                    base, nseg, lds, s)                      \
+                                    base, nseg, lds, s, wave_all)            \
        : launch_list_t<M, false, TX>(X, d, ldx, k, v, lab_out, acc, amode,   \
-                                     base, nseg, lds, s))
+                                     base, nseg, lds, s, wave_all))
   const int r = maxd == 32 ? DKM_LL(32) : maxd == 64 ? DKM_LL(64) : DKM_LL(128);
 #undef DKM_LL
   return r;
@@ -3216,7 +3221,7 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
       return r;
     if ((use_list || b1) && (r = launch_list<TX>(X, d, ldx, k, v, lab_out,
                                                   acc, skind, vec, base,
-                                                  nseg, s)))
+                                                  nseg, s, sub)))
       return r;
     if ((r = launch_recheck<TX>(X, end, d, ldx, k, v, lab_out, acc,
                                 skind, vec, base, s)))

@@ -58,6 +58,7 @@ for s in "$@"; do
     t_all) step t_all 1100 $PT -m gpu tests ;;
     diag) step diag 300 python tools/c3_diag.py; cat $OUT/${TAG}_diag.log | cut -c1-300 ;;
     rsdiag) step rsdiag 300 python tools/rescreen_diag.py; cat $OUT/${TAG}_rsdiag.log | cut -c1-300 ;;
+    rstrace) trace rstrace 300 python tools/rescreen_diag.py ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py; summ $OUT/${TAG}_bench.log ;;
     prof) trace prof 600 python bench.py --no-cpu ;;
