@@ -2134,16 +2134,28 @@ __device__ __forceinline__ void resolve_wave(
     xf[t] = t < d ? (float)ld_x(xr + t) : 0.f;
     xx = fmaf(xf[t], xf[t], xx);
   }
+  // the centre's fp32 row (dp floats, 16-B aligned) by 16-B loads, all
+  // issued before the fma chain (the same chain order as resolve_lane)
   auto score = [&](int jc) {
-    const float *cr = cl + (int64_t)jc * dp;
+    const f32x4 *cr = (const f32x4 *)(cl + (int64_t)jc * dp);
+    f32x4 c4[MAXD / 4];
+#pragma unroll
+    for (int t4 = 0; t4 < MAXD / 4; ++t4)
+      if (4 * t4 < dp) c4[t4] = cr[t4];
     float dot = 0.f;
 #pragma unroll
-    for (int t = 0; t < MAXD; ++t)
-      if (t < dp) dot = fmaf(xf[t], cr[t], dot);
+    for (int t4 = 0; t4 < MAXD / 4; ++t4)
+      if (4 * t4 < dp) {
+        dot = fmaf(xf[4 * t4 + 0], c4[t4].x, dot);
+        dot = fmaf(xf[4 * t4 + 1], c4[t4].y, dot);
+        dot = fmaf(xf[4 * t4 + 2], c4[t4].z, dot);
+        dot = fmaf(xf[4 * t4 + 3], c4[t4].w, dot);
+      }
     return fmaf(-2.f, dot, cnl[jc]);
   };
   float b1 = INFINITY, b2 = INFINITY;
   int i1 = INT32_MAX;
+#pragma unroll 2
   for (int jc = lane; jc < k; jc += 64) {
     const float sc = score(jc);
     i1 = sc < b1 ? jc : i1;
@@ -3052,11 +3064,17 @@ static int rescreen_list(const TX *X, int d, int64_t ldx, const double *C,
   if (nseg <= 0) return 0;
   k_list_scan<<<1, 1024, 0, s>>>(v.tcount, nseg, v.rprefix, &v.hdr->rtotal);
   if (int r = check_launch("re-screen: list scan")) return r;
-  uint32_t tot = 0;
-  if (hipMemcpyAsync(&tot, &v.hdr->rtotal, 4, hipMemcpyDeviceToHost, s) !=
+  // the length through pinned host memory (a pageable read stalled the
+  // stream for ~3 ms once per process in the C3 trace)
+  static thread_local uint32_t *pinned = nullptr;
+  if (!pinned && hipHostMalloc((void **)&pinned, 64, hipHostMallocDefault) !=
+                     hipSuccess)
+    return fail(DKM_E_LAUNCH, "re-screen: pinned buffer");
+  if (hipMemcpyAsync(pinned, &v.hdr->rtotal, 4, hipMemcpyDeviceToHost, s) !=
           hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return fail(DKM_E_LAUNCH, "re-screen: list length");
+  const uint32_t tot = *pinned;
   if (tot == 0) return 0;
   const int cus = dev_info().cus;
   k_list_compact<<<(unsigned)std::min<int64_t>((nseg + 3) / 4, cus * 8), 256,
