@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("DKM_LIB", os.path.join(_HERE, "libdkm.so"))
 # constants mirrored from include/dkm.h
 ABI_VERSION = 3
 MODE_AUTO, MODE_EXACT, MODE_SCREEN32, MODE_BF16X3, MODE_BF16 = 0, 1, 2, 3, 4
-MODE_MASK, MODE_NOHINT, MODE_B1 = 0xff, 0x100, 0x200
+MODE_MASK, MODE_NOHINT, MODE_B1, MODE_TRANSLATE = 0xff, 0x100, 0x200, 0x400
 IMAGE_NONE, IMAGE_SINGLE, IMAGE_SPLIT, IMAGE_SORTED, IMAGE_GEMM = 0, 1, 2, 3, 4
 IMAGE_BUILD = 0x100   # kind flag: build the allocated image during the call
 SUMS_F64, SUMS_F32, SUMS_RECIP = 0, 1, 2

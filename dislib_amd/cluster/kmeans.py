@@ -164,6 +164,10 @@ REFRESH = 64
 # without it (the tests switch it off through this module attribute).
 SORTED_IMAGE = True
 SORT_AT = 1
+# the first assignment of a label-sorted-image fit: the single-product
+# screen over translated centres (DKM_MODE_TRANSLATE) instead of bf16x3
+# (labels are identical either way; the tests switch it)
+TRANSLATE_FIRST = True
 
 
 class _Lloyd:
@@ -251,10 +255,18 @@ class _Lloyd:
         mode = self.mode
         image = None
         if mode == _lib.MODE_AUTO and self.it == 0:
-            # the first iteration scores against the initial centres, where
-            # the single-product screen the library picks for large k x d
-            # would leave most samples undecided -- screen it with bf16x3
-            mode = _lib.MODE_BF16X3
+            # the first iteration scores against the initial centres
+            # (U[0, 1)^d, crowded): the plain single-product screen would
+            # leave most samples undecided.  The shapes of the label-sorted
+            # image take it with the translated centres (DKM_MODE_TRANSLATE:
+            # the bf16 error scales with max ||c - mean||, and k_cand2 / the
+            # bf16x3 re-screen take what it leaves); the others screen with
+            # bf16x3
+            if self.sorting and TRANSLATE_FIRST:
+                mode = _lib.MODE_BF16 | _lib.MODE_NOHINT | \
+                    _lib.MODE_TRANSLATE
+            else:
+                mode = _lib.MODE_BF16X3
             if self.sorting:
                 image = (None, 0)
         elif self.sorting:

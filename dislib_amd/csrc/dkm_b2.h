@@ -57,12 +57,16 @@ struct B2View {
   // min_{j in block cb, j != p} |c_p - c_j| (dkm_util.hip k_mind); nullptr
   // = no skipping
   const float *mind;
+  // DKM_MODE_TRANSLATE: b1frag holds -2 (c - m); the bound's x.c magnitude
+  // term takes max ||c - m|| (hdr->umax_bits) instead of max ||c||
+  int transl;
 };
 
-inline B2View b2_view(const WsView &v, bool sorted) {
+inline B2View b2_view(const WsView &v, bool sorted, bool transl = false) {
   B2View bv;
   bv.hdr = v.hdr;
-  bv.b1frag = v.b1frag;
+  bv.b1frag = transl ? v.b1frag_t : v.b1frag;
+  bv.transl = transl ? 1 : 0;
   bv.cn32f = v.cn32f;
   bv.cn32 = v.cn32;
   bv.tlist = v.tlist;

@@ -117,6 +117,14 @@ __global__ void __launch_bounds__(SB2)
   // top-3 fallback: b1's packed single-product bound
   const float rel = 1.02f * 0x1.0p-8f + (16.0f * NKS + 2.0f) * 0x1.0p-23f;
   BoundK bk = bound_consts<P_F32>(d, cm);
+  if (v.transl) {
+    // the products are x . (-2 (c - m)): their magnitude term takes
+    // max ||c - m||; |c|^2 and the reference's rounding keep cm
+    const float um =
+        (float)__longlong_as_double((long long)v.hdr->umax_bits) * 1.000001f;
+    bk.two_cm = __int_as_float(
+        __builtin_amdgcn_readfirstlane(__float_as_int(2.0f * um)));
+  }
   bk.k_mag = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(
       2.0f * (2.0f * rel + 0x1.0p-23f * (float)(1u << PACK2)) * 1.0001f)));
   // threshold pass: no packing, the chain over |T| + sum |x c| (see top)
@@ -1468,7 +1476,8 @@ int launch_plab_sync(const XImage &img, int64_t n, int k, const int32_t *lab,
 template <class TX>
 int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
                      const WsView &v, int32_t *lab_out, int64_t base, int hint,
-                     int cus, hipStream_t s, int *nseg, XImage img) {
+                     int cus, hipStream_t s, int *nseg, XImage img,
+                     bool transl) {
   const size_t lds = b2_lds_bytes(k, d);
   if (lds > 160 * 1024) return 1;  // caller uses k_screen_b1
   // the image paths read whole tiles: the range must start on one (the
@@ -1476,6 +1485,9 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
   int ik = img.tiles ? img.kind : IMG_NONE;
   if (ik == IMG_SORTED && base != 0)
     return fail(DKM_E_ARG, "screen_b2: the sorted image needs the whole range");
+  if (ik == IMG_SORTED && transl)
+    return fail(DKM_E_ARG, "screen_b2: no translation over the sorted image");
+  if (transl && !v.b1frag_t) transl = false;
   if (ik == IMG_SINGLE && base % 32 != 0) ik = IMG_NONE;
   if (ik != IMG_SINGLE && ik != IMG_SORTED) ik = IMG_NONE;
   // the steady state over the sorted image: k_screen_sorted, then this
@@ -1527,7 +1539,7 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
     *nseg =
         (int)std::min<int64_t>((int64_t)g * nw, std::min(TL_SEGS, B1_SEGS));
   }
-  const B2View bv = b2_view(v, ik == IMG_SORTED);
+  const B2View bv = b2_view(v, ik == IMG_SORTED, transl);
   hipLaunchKernelGGL((void (*)(const TX *, int64_t, int, int64_t, int, B2View,
                                int32_t *, int64_t, int, XImage,
                                const int32_t *, const uint32_t *))kf,
@@ -1538,10 +1550,11 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
 
 template int launch_screen_b2<double>(const double *, int64_t, int, int64_t,
                                       int, const WsView &, int32_t *, int64_t,
-                                      int, int, hipStream_t, int *, XImage);
+                                      int, int, hipStream_t, int *, XImage,
+                                      bool);
 template int launch_screen_b2<float>(const float *, int64_t, int, int64_t, int,
                                      const WsView &, int32_t *, int64_t, int,
-                                     int, hipStream_t, int *, XImage);
+                                     int, hipStream_t, int *, XImage, bool);
 
 }  // namespace dkm
 

@@ -3042,7 +3042,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                          size_t wsb, int32_t *labels, double *acc,
                          int acc_kind, hipStream_t s, XImage img,
                          bool nohint = false, bool force_b1 = false,
-                         void *build_img = nullptr, bool sub = false);
+                         void *build_img = nullptr, bool sub = false,
+                         bool transl = false);
 
 // The samples a screen left to the exact re-check (its per-wave lists) are
 // gathered, RS_ROWS at a time, and screened again by the chunked bf16x3
@@ -3112,12 +3113,16 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                          size_t wsb, int32_t *labels, double *acc,
                          int acc_kind, hipStream_t s, XImage img,
                          bool nohint, bool force_b1, void *build_img,
-                         bool sub) {
+                         bool sub, bool transl) {
   (void)wsb;
   const int64_t nq = std::min<int64_t>(v.nq, INT32_MAX);
   if (!labels && nq < 1)
     return fail(DKM_E_WORKSPACE, "screen: no label scratch");
-  const int64_t chunk = labels ? n : nq;
+  // DKM_MODE_TRANSLATE (a fit's first assignment against crowded initial
+  // centres): many samples keep two or more candidates, so the call runs in
+  // row chunks that keep the per-wave lists within their capacity
+  const int64_t chunk =
+      labels ? (transl ? std::min<int64_t>(n, TRANSL_CHUNK) : n) : nq;
   const bool vec = (d % 8 == 0) && (ldx % (16 / (int64_t)sizeof(TX)) == 0) &&
                    (((uintptr_t)X % 16) == 0);
   // single-product screen: labels only, so the sums must come from
@@ -3201,7 +3206,8 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
       const int hint = labels && acc_kind != 0 && !nohint ? 1 : 0;
       r = force_b1 ? 1
                    : launch_screen_b2<TX>(X, end, d, ldx, k, v, lab_out, base,
-                                          hint, dev_info().cus, s, &nseg, img);
+                                          hint, dev_info().cus, s, &nseg, img,
+                                          transl);
       if (r == 1 && img.kind == IMG_SORTED)
         return fail(DKM_E_ARG, "screen: the sorted image needs k_screen_b2");
       if (r == 1)
@@ -3321,7 +3327,8 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
   if (!labels && !acc)
     return fail(DKM_E_ARG, std::string(who) + ": nothing to write");
   hipStream_t s = (hipStream_t)stream;
-  if (mode & ~(DKM_MODE_MASK | DKM_MODE_NOHINT | DKM_MODE_B1))
+  if (mode & ~(DKM_MODE_MASK | DKM_MODE_NOHINT | DKM_MODE_B1 |
+               DKM_MODE_TRANSLATE))
     return fail(DKM_E_ARG, std::string(who) + ": unknown mode flags");
   // DKM_IMAGE_BUILD: build the (allocated, unbuilt) image during this call
   const bool build = image && (image_kind & DKM_IMAGE_BUILD);
@@ -3331,6 +3338,7 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                                ": the sorted image is built by "
                                "dkm_x_image_sorted_*");
   const bool nohint = mode & DKM_MODE_NOHINT, force_b1 = mode & DKM_MODE_B1;
+  bool transl = mode & DKM_MODE_TRANSLATE;
   mode &= DKM_MODE_MASK;
   if (mode == DKM_MODE_AUTO)
     mode = !screen_ok(k, d) && !gemm_path(k, d) ? DKM_MODE_EXACT
@@ -3389,10 +3397,13 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
     const XImage img = image ? x_image_view(image, n, d, image_kind)
                              : XImage{nullptr, nullptr, IMG_NONE, nullptr,
                                       nullptr};
+    // the translated centres serve the single-product screen without the
+    // sorted image (its block skipping reads absolute scores)
+    if (image_kind == IMG_SORTED || prec != P_B1) transl = false;
     return launch_screen<TX>(prec, X, n, (int)d, ldx, C, (int)k, v, wsb,
                              labels, acc, acc_kind, s, img, nohint, force_b1,
                              build && split_w32 ? (void *)image : nullptr,
-                             false);
+                             false, transl);
   }
   return fail(DKM_E_ARG, std::string(who) + ": bad mode");
 }

@@ -77,6 +77,7 @@ struct WsHeader {
   int32_t lseg;    // list segments of the last single-product screen launch
   int32_t pad3;
   uint64_t sfall_total;
+  uint64_t umax_bits;  // max_c ||c - m||_2 (m: b1frag_t's translation)
 };
 constexpr uint64_t WS_MAGIC = 0x444b4d5753303034ull;  // "DKMWS004"
 constexpr size_t WS_HDR = 256;
@@ -130,6 +131,10 @@ inline bool b1_ok(int64_t k, int64_t d) {
 // bf16x3 screen with its two-candidate list.  Shapes of the single-product
 // screens with rows k_cand2 takes; RS_ROWS rows per gathered chunk.
 constexpr int64_t RS_ROWS = 262144;
+// DKM_MODE_TRANSLATE calls run in chunks of this many rows (the per-wave
+// two-candidate and re-check lists of k_screen_b2: ~18 % and ~5 % of the
+// rows against the reference's U[0, 1) initial centres at C3's shape)
+constexpr int64_t TRANSL_CHUNK = 1ll << 25;
 inline bool rescreen_ok(int64_t k, int64_t d) {
   return b1_ok(k, d) && d % 8 == 0 && d >= 8;
 }
@@ -160,6 +165,10 @@ struct WsView {
   float *cnpad;   // kpad16 fp32 ||c||^2, 2^100 for padding centres
   uint16_t *bfrag; // bf16 hi/lo of -2*centres, 16x16x32 fragment order
   uint16_t *b32frag; // d <= 32: bf16 hi/lo, 32x32x16 order (k_screen_w32)
+  // b1_ok: b1frag of the translated centres -2 (c - m), m = mvec (fp32, the
+  // centres' mean per feature; DKM_MODE_TRANSLATE)
+  uint16_t *b1frag_t;
+  float *mvec;
   float *cn32f;   // kpad32 ||c||^2 in 32x32 accumulator order
   uint16_t *b1frag; // b1_ok: bf16 hi of -2c, 32x32x16 order, dpad16 / 16
                     // K-steps per 32-centre block (k_screen_b1)
@@ -267,7 +276,7 @@ template <class TX>
 int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
                      const WsView &v, int32_t *lab_out, int64_t base,
                      int hint, int cus, hipStream_t s, int *nseg,
-                     XImage img);
+                     XImage img, bool transl = false);
 
 // Two-candidate samples of the single-product screens (dkm_cand.hip):
 // the reference arithmetic on both listed centres.  1 = not launched

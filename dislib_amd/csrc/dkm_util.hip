@@ -68,6 +68,8 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
   b += gemm_bytes(k, d);
   if (b1_ok(k, d)) {
     b += round_up(kpad32(k) * dpad16(d) * 2, 256);  // b1frag
+    b += round_up(kpad32(k) * dpad16(d) * 2, 256);  // b1frag_t
+    b += round_up(d * 4, 256);                      // mvec
     b += (size_t)B1_SEGS * B1_CAP * 8;              // clist
     b += (size_t)B1_SEGS * 4;                       // ccount
     b += (size_t)B1_SEGS * B1_NCAP * 16;            // nlist
@@ -129,6 +131,8 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   v->gpart = nullptr;
   v->gchunk = 0;
   v->b1frag = nullptr;
+  v->b1frag_t = nullptr;
+  v->mvec = nullptr;
   v->clist = nullptr;
   v->ccount = nullptr;
   v->nlist = nullptr;
@@ -156,6 +160,10 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   if (b1_ok(k, d)) {
     v->b1frag = (uint16_t *)p;
     p += round_up(kpad32(k) * dpad16(d) * 2, 256);
+    v->b1frag_t = (uint16_t *)p;
+    p += round_up(kpad32(k) * dpad16(d) * 2, 256);
+    v->mvec = (float *)p;
+    p += round_up(d * 4, 256);
     v->clist = (int2 *)p;
     p += (size_t)B1_SEGS * B1_CAP * 8;
     v->ccount = (int32_t *)p;
@@ -210,6 +218,7 @@ __global__ void k_ws_header(WsHeader *h, int64_t k, int64_t d, int64_t dpad,
     h->dpad = dpad;
     h->n_queue = n_queue;
     h->cmax_bits = 0;
+    h->umax_bits = 0;
     h->qcount = 0;  // rechecked_total accumulates over the workspace life
   }
 }
@@ -257,6 +266,39 @@ __global__ void __launch_bounds__(256) k_prepare(const double *__restrict__ C,
     // non-negative doubles order like their bit patterns
     atomicMax((unsigned long long *)&v.hdr->cmax_bits,
               (unsigned long long)__double_as_longlong(nrm));
+  }
+  if (v.mvec) {
+    // ||c - m|| for DKM_MODE_TRANSLATE's bound (any order: it bounds the
+    // bf16 operands' magnitudes, rounded up by the kernels' 1.000001)
+    __syncthreads();
+    double u2 = 0.0;
+    for (int64_t t = threadIdx.x; t < d; t += blockDim.x) {
+      const double u = row[t] - (double)v.mvec[t];
+      u2 += u * u;
+    }
+    srow[threadIdx.x] = u2;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (threadIdx.x < off) srow[threadIdx.x] += srow[threadIdx.x + off];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0)
+      atomicMax((unsigned long long *)&v.hdr->umax_bits,
+                (unsigned long long)__double_as_longlong(
+                    sqrt(srow[0]) * (1.0 + 0x1.0p-40)));
+  }
+}
+
+// DKM_MODE_TRANSLATE's m: the centres' mean per feature, rounded to fp32
+// (any m keeps the screen exact; the mean makes max ||c - m|| small)
+__global__ void __launch_bounds__(256) k_mvec(const double *__restrict__ C,
+                                              int64_t k, int64_t d,
+                                              float *__restrict__ m) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < d;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    double a = 0.0;
+    for (int64_t c = 0; c < k; ++c) a += C[c * d + t];
+    m[t] = (float)(a / (double)k);
   }
 }
 
@@ -317,6 +359,11 @@ __global__ void __launch_bounds__(256) k_frag(const double *__restrict__ C,
       const double x = (c < k && t < d) ? -2.0 * C[c * d + t] : 0.0;
       v.b1frag[blk * 512 + l * 8 + j] =
           __builtin_bit_cast(uint16_t, (__bf16)(float)x);
+      // the translated centres: -2 (c - m) rounded the same way
+      const double xt =
+          (c < k && t < d) ? -2.0 * (C[c * d + t] - (double)v.mvec[t]) : 0.0;
+      v.b1frag_t[blk * 512 + l * 8 + j] =
+          __builtin_bit_cast(uint16_t, (__bf16)(float)xt);
     }
   }
   if (d > 32) return;
@@ -526,6 +573,11 @@ int dkm_prepare_centers(const double *C, int64_t k, int64_t d, int flags,
   hipStream_t s = (hipStream_t)stream;
   const int64_t dpad = round_up(d, 4);
   k_ws_header<<<1, 64, 0, s>>>(v.hdr, k, d, dpad, v.nq);
+  if (v.mvec && !(flags & DKM_PREP_CSR))
+    k_mvec<<<(unsigned)std::max<int64_t>(1, (d + 255) / 256), 256, 0, s>>>(
+        C, k, d, v.mvec);
+  else
+    v.mvec = nullptr;   // (a local copy: k_prepare skips ||c - m||)
   k_prepare<<<(unsigned)k, 256, 0, s>>>(C, k, d, dpad, flags, v);
   if (!(flags & DKM_PREP_CSR)) {  // the dense screens' centre tiles
     const int64_t tot = (kpad16(k) / 16) * (dpad32(d) / 32) * 512;

@@ -61,6 +61,16 @@ extern "C" {
                                centres-on-rows form (k_screen_b1, the
                                fallback when k_screen_b2's LDS image does
                                not fit) for every shape; identical labels */
+#define DKM_MODE_TRANSLATE 0x400 /* with DKM_MODE_SCREEN_BF16 (or the AUTO
+                               choice of it), no sorted image: the centres-
+                               on-lanes screen scores ||c||^2 - 2 x.(c - m)
+                               with m the centres' mean (the same order of
+                               the centres for every sample; x.m is common to
+                               all of them), so its bf16 rounding error
+                               scales with max ||c - m|| instead of
+                               max ||c||: crowded centres (the reference's
+                               U[0, 1) initial centres) leave far fewer
+                               samples to the re-checks.  Labels identical */
 
 /* sum-dtype flags for dkm_update_centers (reference keeps X's dtype for the
  * partial sums; base.py:178 and :147) */

@@ -289,3 +289,64 @@ def test_fit_shapes_without_the_sorted_image(d, ldx):
     assert np.array_equal(got, lab), (got != lab).sum()
     err = np.max(np.abs(st.C.cpu().numpy() - C) / np.maximum(np.abs(C), 1.0))
     assert err <= 1e-9
+
+
+@pytest.mark.parametrize("shift,spread", [(0.0, 1.0), (50.0, 1.0),
+                                          (-3.0, 0.01)])
+def test_translated_single_product_screen_vs_oracle(shift, spread):
+    """DKM_MODE_TRANSLATE: the centres-on-lanes single-product screen over
+    -2 (c - m) (m = the centres' mean) with the bound's x.c term on
+    max ||c - m||: labels equal the oracle's for crowded centres far from the
+    origin (shift), tight crowds (spread) and the reference's U[0, 1) init,
+    with the sums / counts of the same assignment."""
+    from dislib_amd import _device, _lib
+    from dislib_amd.data import load_data
+    rng = np.random.default_rng(int(abs(shift) * 7 + spread * 100))
+    n, d, k = 60000, 64, 1000
+    blobs = rng.uniform(-10, 10, (50, d)) + shift
+    x = blobs[rng.integers(0, 50, n)] + rng.standard_normal((n, d))
+    C = shift + spread * rng.random((k, d))
+    dev = torch.device("cuda", 0)
+    dd = load_data(x, subset_size=n)._device_data()
+    ws = _device.Workspace(k, d, n, dev)
+    acc = torch.zeros(k * (d + 1), dtype=torch.float64, device=dev)
+    Ct = torch.from_numpy(C).to(dev)
+    lab = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    _device.prepare(Ct, ws, acc)
+    mode = _lib.MODE_BF16 | _lib.MODE_NOHINT | _lib.MODE_TRANSLATE
+    _device.partial_sum(dd, Ct, ws, lab, acc, mode)
+    rl, rs, rc = orc.partial_sum(x, C)
+    assert np.array_equal(lab.cpu().numpy(), rl)
+    a = acc.cpu().numpy()
+    assert np.array_equal(a[k * d:], rc.astype(np.float64))
+    err = np.max(np.abs(a[:k * d].reshape(k, d) - rs) /
+                 np.maximum(np.abs(rs), 1.0))
+    assert err <= 1e-11
+
+
+def test_translated_first_iteration_fit_matches(monkeypatch):
+    """A label-sorted-image fit whose first assignment takes the translated
+    single-product screen equals the bf16x3 first assignment: labels,
+    centres and iteration count (400k x 64, k = 1000, device blobs)."""
+    from dislib_amd import _device
+    from dislib_amd.cluster.kmeans import _Lloyd, _init_centers
+    from dislib_amd.data import Dataset, Subset
+    import dislib_amd.cluster.kmeans as km_mod
+    n, d, k = 400_000, 64, 1000
+    dev = torch.device("cuda", 0)
+    X = torch.empty((n, d), dtype=torch.float64, device=dev)
+    _device.make_blobs(X, 0, k, seed=3, box=10.0, std=1.0)
+    out = {}
+    for on in (False, True):
+        monkeypatch.setattr(km_mod, "TRANSLATE_FIRST", on)
+        ds = Dataset(n_features=d)
+        ds.append(Subset(X))
+        st = _Lloyd(ds, _init_centers(d, False, k, 3), 0.0, True, "auto",
+                    dev)
+        for _ in range(4):
+            st.step()
+        out[on] = (st.labels[:n].cpu().numpy(), st.C.cpu().numpy())
+    assert np.array_equal(out[True][0], out[False][0])
+    err = np.max(np.abs(out[True][1] - out[False][1]) /
+                 np.maximum(np.abs(out[False][1]), 1.0))
+    assert err <= 1e-12
