@@ -165,9 +165,13 @@ REFRESH = 64
 SORTED_IMAGE = True
 SORT_AT = 1
 # the first assignment of a label-sorted-image fit: the single-product
-# screen over translated centres (DKM_MODE_TRANSLATE) instead of bf16x3
-# (labels are identical either way; the tests switch it)
-TRANSLATE_FIRST = True
+# screen over translated centres (DKM_MODE_TRANSLATE) instead of bf16x3.
+# Off: at C3 the translated screen still leaves ~40 % of the rows two or
+# more candidates against the U[0, 1) centres (its 2B window is 4 x 2^-8
+# x |x| max |c - m|), and the iteration took 93 ms against bf16x3's 73.5
+# (profiles/r06/c3/r06h_translate_iters.txt).  Labels are identical either
+# way; the tests run both.
+TRANSLATE_FIRST = False
 
 
 class _Lloyd:
