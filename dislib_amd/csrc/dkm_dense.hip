@@ -2325,9 +2325,11 @@ __global__ void __launch_bounds__(BLOCK)
                                 v.cn32, dp,
                                 cm, v.ct64, lab_out, amode, at);
   };
-  // stage-2 samples go to the global list that k_recheck_wave resolves a
-  // wave per sample (v.smoved as (offset, prev) pairs; the per-wave LDS
-  // list only takes what overflows it)
+  // wave_all: the samples go to the global list that k_recheck_wave
+  // resolves a wave per sample (v.smoved as (offset, prev) pairs; the
+  // per-wave LDS list only takes what overflows it).  Otherwise stage 1 runs
+  // here lane per sample and its leftovers are resolved 64 at a time (a long
+  // list holds many of them: a wave per sample cost 0.7 ms per C2 iteration)
   int2 *s2l = (int2 *)v.smoved;
   const uint32_t s2cap = (uint32_t)std::min<int64_t>(v.nq / 2, INT32_MAX);
 #if DKM_LIST_SPREAD
@@ -2360,7 +2362,7 @@ __global__ void __launch_bounds__(BLOCK)
                                                v.ct64, lab_out, amode, at);
       }
       unsigned long long m = __ballot(!ok);
-      if (m) {
+      if (m && wave_all) {
         uint32_t pos = 0;
         if (lane == 0) pos = atomicAdd(&v.hdr->s2count, (uint32_t)__popcll(m));
         pos = (uint32_t)__shfl((int)pos, 0, 64);
@@ -2734,9 +2736,10 @@ static int launch_list_t(const TX *X, int d, int64_t ldx, int k,
   k_recheck_list<MAXD, VEC, TX><<<(unsigned)g, BLOCK, lds, s>>>(
       X, d, ldx, k, v, lab_out, acc, amode, base, nseg, wave_all ? 1 : 0);
   if (int r = check_launch("list re-check")) return r;
+  if (!wave_all) return 0;
   k_recheck_wave<MAXD, TX><<<(unsigned)(dev_info().cus * 4), BLOCK, 0, s>>>(
       X, d, ldx, k, v, lab_out, acc, amode, base);
-  return check_launch("list re-check (stage 2, wave per sample)");
+  return check_launch("list re-check (wave per sample)");
 }
 
 // Can the listed samples be resolved lane-per-sample (k_recheck_list)?
