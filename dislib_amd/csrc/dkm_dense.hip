@@ -342,6 +342,7 @@ __global__ void __launch_bounds__(BLOCK)
 }  // namespace dkm
 
 #include "dkm_screen.h"
+#include "dkm_b2.h"
 
 namespace dkm {
 
@@ -1064,7 +1065,20 @@ __device__ __forceinline__ void wave_sync_w() {
 #ifndef DKM_W32_WPE
 #define DKM_W32_WPE 3
 #endif
-template <class TX, bool IMG>
+// HINT (image delta launches, k <= W32_HINT_KMAX: the steady iterations of
+// C2): a threshold pass, as k_screen_b2's.  With p = the row's incoming
+// label, s_hat_p comes from v_dot2 products of the same bf16x3 operands
+// (within the bound of the MFMA scores), T = s_hat_p + 2B, and a centre
+// whose score exceeds T can neither win nor tie.  Each 32-centre block is
+// tested as a whole -- one min over the 16 accumulators against T -- and
+// only a block with some score <= T (rare once labels settle) runs the
+// packed top-2 update; p's own accumulator starts from +2^100 (a poisoned
+// copy of its norm chunk), so p's block does not hit on p itself.  Per
+// score: about 0.6 VALU instead of the top-2's 3 (VALU:MFMA 13:1, the
+// limit of this kernel, round-5 PMC).  The decision over {p} and the kept
+// scores is the same rule, exactly: every centre left out is > T.
+constexpr int W32_HINT_KMAX = 256;
+template <class TX, bool IMG, bool HINT = false>
 __global__ void __launch_bounds__(SBW) __attribute__((
     amdgpu_waves_per_eu(DKM_W32_WPE)))
     k_screen_w32(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
@@ -1092,6 +1106,20 @@ __global__ void __launch_bounds__(SBW) __attribute__((
   const bool full_acc = am_full(amode);
   const bool delta = amode & AM_DELTA;
   const AccTarget at = acc_target(amode, lds_acc, acc, k, d);
+  char *scr0 = (char *)((amode & AM_INLDS) ? lds_acc + lds_acc_len(k, d)
+                                           : lds_acc);
+  // HINT: centre p's norm chunk (the 16 norms of its block half) with p's
+  // own slot +2^100, 16 floats per centre, in place of the waves' scratch
+  // (the image launches use none)
+  float *pcn = (float *)scr0;
+  if constexpr (HINT) {
+    for (int e = threadIdx.x; e < k * 16; e += SBW) {
+      const int p = e >> 4, g = e & 15, q = p & 31;
+      const int gp = (q & 3) | ((q >> 3) << 2);
+      pcn[e] = g == gp ? 0x1.0p100f
+                       : v.cn32f[(p >> 5) * 32 + 16 * ((q >> 2) & 1) + g];
+    }
+  }
   __syncthreads();
 
   const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
@@ -1099,9 +1127,7 @@ __global__ void __launch_bounds__(SBW) __attribute__((
   // per-wave scratch (W32_SCR bytes) after the accumulators: the transpose
   // of one 16-feature half of the tile (bf16 hi then lo, 32 rows x 32 B
   // each), |x|^2 per sample, the decided labels (full sums)
-  char *scr = (char *)((amode & AM_INLDS) ? lds_acc + lds_acc_len(k, d)
-                                          : lds_acc) +
-              wid * W32_SCR;
+  char *scr = scr0 + wid * W32_SCR;
   char *s_hi = scr, *s_lo = scr + 1024;
   float *s_xx = (float *)(scr + 2048);
   int *s_lab = (int *)(scr + 2176);
@@ -1277,8 +1303,49 @@ __global__ void __launch_bounds__(SBW) __attribute__((
     float r1 = INFINITY, r2 = INFINITY;
     int ri = 0;
     typedef float f32x16 __attribute__((ext_vector_type(16)));
+    float xn;
+    const float B2 = bound2_fast(bk, xx, xn);
+    // HINT: p, s_hat_p (v_dot2 over this lane's 16 features of the bf16x3
+    // operands, the two halves added), T
+    const int p = prv;
+    const bool pok = HINT && p >= 0 && p < k;
+    float shp = INFINITY, T = INFINITY;
+    if constexpr (HINT) {
+      float dg = 0.f;
+      if (pok) {
+        const char *pf = frag + (int64_t)(p >> 5) * 4096 +
+                         ((p & 31) + 32 * h) * 16;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 ch = *(const bf16x8 *)(pf + ks * 2048);
+          const bf16x8 cl = *(const bf16x8 *)(pf + ks * 2048 + 1024);
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            const bf16x2 c2h{ch[j], ch[j + 1]};
+            dg = __builtin_amdgcn_fdot2_f32_bf16(
+                bf16x2{xh[ks][j], xh[ks][j + 1]}, c2h, dg, false);
+            dg = __builtin_amdgcn_fdot2_f32_bf16(
+                bf16x2{xl[ks][j], xl[ks][j + 1]}, c2h, dg, false);
+            dg = __builtin_amdgcn_fdot2_f32_bf16(
+                bf16x2{xh[ks][j], xh[ks][j + 1]}, bf16x2{cl[j], cl[j + 1]},
+                dg, false);
+          }
+        }
+      }
+      float da, db;
+      pair_xor<32>(dg, da, db);
+      dg = da + db;
+      if (pok) {
+        const int q = p & 31;
+        shp = cn[(p >> 5) * 32 + 16 * ((q >> 2) & 1) +
+                 ((q & 3) | ((q >> 3) << 2))] + dg;
+        T = shp + B2;
+      }
+    }
     auto chain = [&](int cb, f32x16 &accv) {
-      const f32x4 *c4p = (const f32x4 *)(cn + cb * 32 + 16 * h);
+      const bool pz = HINT && pok && (p >> 5) == cb && ((p >> 2) & 1) == h;
+      const f32x4 *c4p =
+          (const f32x4 *)(pz ? pcn + p * 16 : cn + cb * 32 + 16 * h);
       const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
       accv = f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
                     c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
@@ -1295,7 +1362,40 @@ __global__ void __launch_bounds__(SBW) __attribute__((
                                                        0);
       }
     };
-    for (int g0 = 0; g0 < nkb; g0 += GB) {
+    if constexpr (HINT) {
+      // the threshold pass: a block with no score <= T is done in 8 VALU
+      auto test = [&](int cb, const f32x16 &accv) {
+        const bool hit = min16(accv, ninf) <= T;
+        if (__ballot(hit) == 0) return;
+        if (hit) {
+          float b1 = INFINITY, b2 = INFINITY;
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const float sq =
+                __uint_as_float((__float_as_uint(accv[g]) & vmask) | g);
+            b2 = __builtin_amdgcn_fmed3f(b1, b2, sq);
+            b1 = min_nc(b1, sq, ninf);
+          }
+          const int g = (int)(__float_as_uint(b1) & 15);
+          const int gi = cb * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+          const bool nw = b1 < r1;
+          r2 = nw ? min_nc(r1, b2, ninf) : min_nc(r2, b1, ninf);
+          ri = nw ? gi : ri;
+          r1 = nw ? b1 : r1;
+        }
+      };
+      f32x16 acc_a, acc_b;
+      chain(0, acc_a);
+      int cb = 0;
+      for (; cb + 2 <= nkb; cb += 2) {
+        chain(cb + 1, acc_b);
+        test(cb, acc_a);
+        if (cb + 2 < nkb) chain(cb + 2, acc_a);
+        test(cb + 1, acc_b);
+      }
+      if (cb < nkb) test(cb, acc_a);
+    }
+    for (int g0 = 0; !HINT && g0 < nkb; g0 += GB) {
       const int g1 = min(nkb, g0 + GB);
       float b1 = INFINITY, b2 = INFINITY;
       auto score = [&](int cb, const f32x16 &accv) {
@@ -1337,9 +1437,14 @@ __global__ void __launch_bounds__(SBW) __attribute__((
       ri = tc ? ci : ai;
       r2 = tc ? min_nc(a1, c2, ninf) : min_nc(a2, c1, ninf);
     }
+    if (HINT && pok) {
+      // the kept scores (all <= T) with p's: every other centre is > T
+      const bool tk = (shp < r1) | ((shp == r1) & (p < ri));
+      r2 = tk ? r1 : min_nc(r2, shp, ninf);
+      ri = tk ? p : ri;
+      r1 = tk ? shp : r1;
+    }
     const int64_t si = s0 + r;
-    float xn;
-    const float B2 = bound2_fast(bk, xx, xn);
     const bool sane = (xn < 1e18f) & (xn * cm < 1e30f) & (r1 < 1e30f);
     const bool unique = sane & (r2 - r1 > B2);
     const bool und = si < n && !unique;
@@ -2607,15 +2712,26 @@ static int launch_screen_w32(const TX *X, int64_t end, int d, int64_t ldx,
   // launch (full sums, base 0) writes it instead
   const bool im = !build && img.tiles && img.kind == IMG_SPLIT &&
                   !am_full(amode) && base % 32 == 0;
-  const void *kf = im ? (const void *)k_screen_w32<TX, true>
-                      : (const void *)k_screen_w32<TX, false>;
-  lds += (size_t)(SBW / 64) * W32_SCR;  // the waves' transpose scratch
+  // the waves' transpose scratch: the X-converting launches only (three
+  // blocks per CU need <= 53 KB each)
+  if (!im) lds += (size_t)(SBW / 64) * W32_SCR;
+  // the threshold pass: image delta launches (incoming labels = hints)
+  const size_t pcn_bytes = (size_t)kpad32(k) * 16 * 4;
+  const bool hint = im && (amode & AM_DELTA) && k <= W32_HINT_KMAX &&
+                    lds + pcn_bytes <= LDS_BUDGET;
+  if (hint) lds += pcn_bytes;
+  const void *kf = hint ? (const void *)k_screen_w32<TX, true, true>
+                   : im ? (const void *)k_screen_w32<TX, true>
+                        : (const void *)k_screen_w32<TX, false>;
   const int64_t cap = (int64_t)dev_info().cus * resident_blocks(kf, SBW, lds);
   const int64_t per_block = 32 * (SBW / 64);
   const int64_t need = (end - base + per_block - 1) / per_block;
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min(need, cap));
   *nseg = (int)std::min<int64_t>((int64_t)g * (SBW / 64), TL_SEGS);
-  if (im)
+  if (hint)
+    k_screen_w32<TX, true, true><<<g, SBW, lds, s>>>(
+        X, end, d, ldx, k, v, lab_out, acc, amode, base, use_list, img, 0);
+  else if (im)
     k_screen_w32<TX, true><<<g, SBW, lds, s>>>(X, end, d, ldx, k, v, lab_out,
                                                acc, amode, base, use_list, img,
                                                0);
