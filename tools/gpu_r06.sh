@@ -54,6 +54,7 @@ for s in "$@"; do
   case $s in
     t_new) step t_new 900 $PT tests/test_gpu_dist.py tests/test_gpu_parity.py::test_csr_near_ties_at_the_bf16_table_rounding ;;
     t_core) step t_core 900 $PT tests/test_gpu_image.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py::test_c2_full_size_labels tests/test_gpu_fullsize.py::test_c3_full_size_labels ;;
+    t_w32) step t_w32 900 $PT tests/test_gpu_image.py tests/test_gpu_nonfinite.py tests/test_gpu_parity.py tests/test_gpu_state.py tests/test_gpu_fullsize.py::test_c2_full_size_labels ;;
     t_sorted) step t_sorted 900 $PT tests/test_gpu_sorted.py tests/test_gpu_b2.py tests/test_gpu_fullsize.py::test_c3_full_size_labels ;;
     t_all) step t_all 1100 $PT -m gpu tests ;;
     diag) step diag 300 python tools/c3_diag.py; cat $OUT/${TAG}_diag.log | cut -c1-300 ;;
