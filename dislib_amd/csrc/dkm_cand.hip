@@ -27,8 +27,7 @@ template <class TX, int NST>
 __global__ void __launch_bounds__(CBLOCK)
     k_cand2(const TX *__restrict__ X, int d, int64_t ldx,
             const double *__restrict__ C, WsView v,
-            int32_t *__restrict__ lab_out, int64_t base, int nseg,
-            double *acc, int k, int delta) {
+            int32_t *__restrict__ lab_out, int64_t base, int nseg) {
   const int64_t wv = (int64_t)blockIdx.x * (CBLOCK / 64) + (threadIdx.x >> 6);
   const int64_t nwv = (int64_t)gridDim.x * (CBLOCK / 64);
   const int lane = threadIdx.x & 63;
@@ -73,26 +72,8 @@ __global__ void __launch_bounds__(CBLOCK)
         r2 = r2 + __shfl_xor(r2, off, 64);
       }
       const double q1 = argmin_key(sqrt(r1)), q2 = argmin_key(sqrt(r2));
-      const int win = (q2 < q1 || (q2 == q1 && c2 < c1)) ? c2 : c1;
-      if (acc && live) {
-        // the sums of a screen that accumulates them (k_screen_w32): the
-        // row moves from the previous label (lab_out still holds
-        // -(prev + 2)) to the winner
-        const int prev = delta ? -lab_out[si] - 2 : -1;
-        if (!delta || win != prev) {
-#pragma unroll
-          for (int i = 0; i < NST; ++i) {
-            atomic_add_f64(acc + (int64_t)win * d + j + 8 * i, xv[i]);
-            if (prev >= 0)
-              atomic_add_f64(acc + (int64_t)prev * d + j + 8 * i, -xv[i]);
-          }
-          if (j == 0) {
-            atomic_add_f64(acc + (int64_t)k * d + win, 1.0);
-            if (prev >= 0) atomic_add_f64(acc + (int64_t)k * d + prev, -1.0);
-          }
-        }
-      }
-      if (live && j == 0) lab_out[si] = win;
+      if (live && j == 0)
+        lab_out[si] = (q2 < q1 || (q2 == q1 && c2 < c1)) ? c2 : c1;
     }
   }
   if (mine) atomicAdd((unsigned long long *)&v.hdr->rechecked_total, mine);
@@ -101,8 +82,7 @@ __global__ void __launch_bounds__(CBLOCK)
 template <class TX>
 int launch_cand2_leaf(const TX *X, int d, int64_t ldx, const double *C,
                       const WsView &v, int32_t *lab_out, int64_t base,
-                      int nseg, int cus, hipStream_t s, double *acc, int k,
-                      bool delta) {
+                      int nseg, int cus, hipStream_t s) {
   if (d % 8 != 0 || d < 8 || d > 128) return 1;
   const int64_t units = (int64_t)nseg * (B1_CAP / 64);
   const unsigned g = (unsigned)std::max<int64_t>(
@@ -112,7 +92,7 @@ int launch_cand2_leaf(const TX *X, int d, int64_t ldx, const double *C,
 #define DKM_C2(N)                                                          \
   case N:                                                                  \
     k_cand2<TX, N><<<g, CBLOCK, 0, s>>>(X, d, ldx, C, v, lab_out, base,    \
-                                        nseg, acc, k, delta ? 1 : 0);      \
+                                        nseg);                             \
     break;
     DKM_C2(1) DKM_C2(2) DKM_C2(3) DKM_C2(4) DKM_C2(5) DKM_C2(6) DKM_C2(7)
     DKM_C2(8) DKM_C2(9) DKM_C2(10) DKM_C2(11) DKM_C2(12) DKM_C2(13)
@@ -127,11 +107,11 @@ int launch_cand2_leaf(const TX *X, int d, int64_t ldx, const double *C,
 template int launch_cand2_leaf<double>(const double *, int, int64_t,
                                        const double *, const WsView &,
                                        int32_t *, int64_t, int, int,
-                                       hipStream_t, double *, int, bool);
+                                       hipStream_t);
 template int launch_cand2_leaf<float>(const float *, int, int64_t,
                                       const double *, const WsView &,
                                       int32_t *, int64_t, int, int,
-                                      hipStream_t, double *, int, bool);
+                                      hipStream_t);
 
 }  // namespace dkm
 

@@ -1135,14 +1135,8 @@ __global__ void __launch_bounds__(SBW) __attribute__((
   const int64_t step = (int64_t)gridDim.x * (SBW / 64) * 32;
   const int64_t seg = wv;
   int2 *wl = v.tlist + seg * TL_CAP;
-  const bool listing = (use_list & 1) && seg < TL_SEGS;
+  const bool listing = use_list && seg < TL_SEGS;
   int tl_cnt = 0, tl_over = 0;
-  // HINT, use_list bit 2: exactly-two-candidate rows -> the candidate list
-  // (k_cand2 resolves them and moves their sums)
-  const bool list2 = HINT && (use_list & 2) && v.clist && seg < B1_SEGS;
-  int2 *cl = list2 ? v.clist + seg * B1_CAP : nullptr;
-  int cl_cnt = 0;
-  const float pinf = __uint_as_float(opaque_u32(0x7f800000u));
 
   // Whole 128-B lines per wave-instruction (tools/membench.hip: loading
   // each lane's own 16 features touched 64 lines per instruction and
@@ -1306,8 +1300,8 @@ __global__ void __launch_bounds__(SBW) __attribute__((
     if (!full_acc && s_next < n) load_tile(s_next);
     }  // !IMG
 
-    float r1 = INFINITY, r2 = INFINITY, r3 = INFINITY;
-    int ri = 0, ri2 = 0;
+    float r1 = INFINITY, r2 = INFINITY;
+    int ri = 0;
     typedef float f32x16 __attribute__((ext_vector_type(16)));
     float xn;
     const float B2 = bound2_fast(bk, xx, xn);
@@ -1374,30 +1368,18 @@ __global__ void __launch_bounds__(SBW) __attribute__((
         const bool hit = min16(accv, ninf) <= T;
         if (__ballot(hit) == 0) return;
         if (hit) {
-          // the block's packed top-3, folded into the running top-3 (the
-          // first two with their centres)
-          float b1 = INFINITY, b2 = INFINITY, b3 = INFINITY;
+          float b1 = INFINITY, b2 = INFINITY;
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
             const float sq =
                 __uint_as_float((__float_as_uint(accv[g]) & vmask) | g);
-            b3 = __builtin_amdgcn_fmed3f(b2, b3, sq);
             b2 = __builtin_amdgcn_fmed3f(b1, b2, sq);
             b1 = min_nc(b1, sq, ninf);
           }
           const int g = (int)(__float_as_uint(b1) & 15);
           const int gi = cb * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
-          const int g2 = (int)(__float_as_uint(b2) & 15);
-          const int gi2 = cb * 32 + (g2 & 3) + 8 * (g2 >> 2) + 4 * h;
           const bool nw = b1 < r1;
-          r3 = min_nc(min_nc(r3, b3, ninf),
-                      min_nc(__builtin_amdgcn_fmed3f(r1, b2, pinf),
-                             __builtin_amdgcn_fmed3f(r2, b1, pinf), ninf),
-                      ninf);
-          const bool s2 = nw ? (b2 < r1) : (b1 < r2);
-          const float v2 = nw ? (s2 ? b2 : r1) : (s2 ? b1 : r2);
-          ri2 = nw ? (s2 ? gi2 : ri) : (s2 ? gi : ri2);
-          r2 = v2;
+          r2 = nw ? min_nc(r1, b2, ninf) : min_nc(r2, b1, ninf);
           ri = nw ? gi : ri;
           r1 = nw ? b1 : r1;
         }
@@ -1444,38 +1426,7 @@ __global__ void __launch_bounds__(SBW) __attribute__((
       ri = nw ? gi : ri;
       r1 = nw ? b1 : r1;
     }
-    if constexpr (HINT) {
-      // merge the two lanes' top-3 (symmetric in the pair)
-      float a1, c1, a2, c2, a3, c3;
-      int ai, ci, aj, cj;
-      pair_xor<32>(r1, a1, c1);
-      pair_xor<32>(r2, a2, c2);
-      pair_xor<32>(r3, a3, c3);
-      pair_xor<32>(ri, ai, ci);
-      pair_xor<32>(ri2, aj, cj);
-      const bool tc = (c1 < a1) | ((c1 == a1) & (ci < ai));
-      const float x = tc ? a1 : c1, y = tc ? c2 : a2;
-      const int xi = tc ? ai : ci, yi = tc ? cj : aj;
-      const bool ty = (y < x) | ((y == x) & (yi < xi));
-      r3 = min_nc(min_nc(a3, c3, ninf),
-                  min_nc(__builtin_amdgcn_fmed3f(a1, c2, pinf),
-                         __builtin_amdgcn_fmed3f(a2, c1, pinf), ninf),
-                  ninf);
-      r1 = tc ? c1 : a1;
-      ri = tc ? ci : ai;
-      r2 = ty ? y : x;
-      ri2 = ty ? yi : xi;
-      if (pok) {
-        // the kept scores (all <= T) with p's: every other centre is > T
-        const bool t1 = (shp < r1) | ((shp == r1) & (p < ri));
-        const bool t2 = !t1 & ((shp < r2) | ((shp == r2) & (p < ri2)));
-        r3 = t1 | t2 ? r2 : min_nc(r3, shp, ninf);
-        r2 = t1 ? r1 : t2 ? shp : r2;
-        ri2 = t1 ? ri : t2 ? p : ri2;
-        r1 = t1 ? shp : r1;
-        ri = t1 ? p : ri;
-      }
-    } else {  // merge the two lanes of a sample (symmetric in the pair)
+    {  // merge the two lanes of a sample (symmetric in the pair)
       float a1, c1, a2, c2;
       int ai, ci;
       pair_xor<32>(r1, a1, c1);
@@ -1486,25 +1437,17 @@ __global__ void __launch_bounds__(SBW) __attribute__((
       ri = tc ? ci : ai;
       r2 = tc ? min_nc(a1, c2, ninf) : min_nc(a2, c1, ninf);
     }
+    if (HINT && pok) {
+      // the kept scores (all <= T) with p's: every other centre is > T
+      const bool tk = (shp < r1) | ((shp == r1) & (p < ri));
+      r2 = tk ? r1 : min_nc(r2, shp, ninf);
+      ri = tk ? p : ri;
+      r1 = tk ? shp : r1;
+    }
     const int64_t si = s0 + r;
     const bool sane = (xn < 1e18f) & (xn * cm < 1e30f) & (r1 < 1e30f);
     const bool unique = sane & (r2 - r1 > B2);
-    // HINT: exactly two candidates -> k_cand2 (its row and sums move there)
-    bool two = false;
-    if constexpr (HINT) {
-      two = list2 && si < n && sane && !unique && (r3 - r1 > B2);
-      const uint64_t mc = __ballot(h == 0 && two);
-      const int addc = __popcll(mc);
-      if (cl_cnt + addc <= B1_CAP) {
-        if (h == 0 && two)
-          cl[cl_cnt + lane_prefix(mc)] =
-              make_int2((int)(si - base), ri | (ri2 << 16));
-        cl_cnt += addc;
-      } else {
-        two = false;
-      }
-    }
-    const bool und = si < n && !unique && !two;
+    const bool und = si < n && !unique;
     const int prev = delta ? prv : -1;
     const uint64_t um = __ballot(h == 0 && und);
     const int add = __popcll(um);
@@ -1567,7 +1510,6 @@ __global__ void __launch_bounds__(SBW) __attribute__((
   }
   if (lane == 0) {
     if (listing) v.tcount[seg] = tl_cnt;
-    if (list2) v.ccount[seg] = cl_cnt;
     if (tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
   }
   if (amode & AM_INLDS) {
@@ -2765,8 +2707,7 @@ static int launch_screen_w32(const TX *X, int64_t end, int d, int64_t ldx,
                              int k, const WsView &v, int32_t *lab_out,
                              double *acc, int amode, int64_t base, size_t lds,
                              int use_list, hipStream_t s, int *nseg,
-                             XImage img, bool build = false,
-                             bool *listed2 = nullptr) {
+                             XImage img, bool build = false) {
   // the image serves launches that need no sums from the raw rows; a build
   // launch (full sums, base 0) writes it instead
   const bool im = !build && img.tiles && img.kind == IMG_SPLIT &&
@@ -2779,10 +2720,6 @@ static int launch_screen_w32(const TX *X, int64_t end, int d, int64_t ldx,
   const bool hint = im && (amode & AM_DELTA) && k <= W32_HINT_KMAX &&
                     lds + pcn_bytes <= LDS_BUDGET;
   if (hint) lds += pcn_bytes;
-  // the threshold pass lists exactly-two-candidate rows for k_cand2
-  const bool c2 = hint && v.clist && d % 8 == 0;
-  if (listed2) *listed2 = c2;
-  if (c2) use_list |= 2;
   const void *kf = hint ? (const void *)k_screen_w32<TX, true, true>
                    : im ? (const void *)k_screen_w32<TX, true>
                         : (const void *)k_screen_w32<TX, false>;
@@ -3399,19 +3336,10 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
       r = launch_cand2<TX>(X, d, ldx, C, v, lab_out, base, nseg, s);
       if (!r && hint) r = launch_candn<TX>(X, d, ldx, C, v, lab_out, base,
                                            nseg, s);
-    } else if (w32) {
-      bool listed2 = false;
+    } else if (w32)
       r = launch_screen_w32<TX>(X, end, d, ldx, k, v, lab_out, acc, amode,
                                 base, lds, use_list, s, &nseg, img,
-                                fuse_build, &listed2);
-      // its two-candidate rows: the reference arithmetic on both, and the
-      // row's move in the sums (delta launches)
-      if (!r && listed2)
-        r = launch_cand2_leaf<TX>(X, d, ldx, C, v, lab_out, base,
-                                  std::min(nseg, B1_SEGS), dev_info().cus, s,
-                                  (amode & AM_ON) ? acc : nullptr, k,
-                                  (amode & AM_DELTA) != 0);
-    }
+                                fuse_build);
     else if (prec == P_F32)
       r = vec ? launch_screen_nks<P_F32, true, TX>(X, end, d, ldx, k, v,
                                                    lab_out, acc, amode, base,

@@ -281,14 +281,10 @@ int launch_screen_b2(const TX *X, int64_t end, int d, int64_t ldx, int k,
 // Two-candidate samples of the single-product screens (dkm_cand.hip):
 // the reference arithmetic on both listed centres.  1 = not launched
 // (d % 8 != 0 or d > 128: the screens never list such samples).
-// acc != NULL: the winner's row is also moved in the packed [sums |
-// counts] (delta: +x to the new label and -x from the previous one, read
-// from lab_out's -(prev + 2), when they differ; else +x), fp64 atomics.
 template <class TX>
 int launch_cand2_leaf(const TX *X, int d, int64_t ldx, const double *C,
                       const WsView &v, int32_t *lab_out, int64_t base,
-                      int nseg, int cus, hipStream_t s, double *acc = nullptr,
-                      int k = 0, bool delta = false);
+                      int nseg, int cus, hipStream_t s);
 
 // Sorted sums: counting sort of the sample indices by label (LDS histograms
 // of k bins: k <= SORT_KMAX), then segmented row sums.
