@@ -43,7 +43,7 @@ C2="python bench.py --steps 20 --warmup 3 --no-cpu --only-headline"
 trace() {  # name limit cmd...
   local name=$1 lim=$2; shift 2
   P=$OUT/${TAG}_$name; mkdir -p $P
-  step $name $lim rocprofv3 --kernel-trace --stats -d $P -o run -- "$@"
+  step $name $lim rocprofv3 --kernel-trace --stats -f csv rocpd -d $P -o run -- "$@"
   DB=$(find $P -name '*.db' | head -1)
   [ -n "$DB" ] && python tools/prof_iters.py $DB > $P/iters.txt 2>&1 && rm -f $DB
   find $P -type f ! -name 'iters.txt' ! -name '*kernel_stats.csv' -delete
