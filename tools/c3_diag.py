@@ -4,6 +4,11 @@ tile's first label, centre blocks screened and tiles handed to the general
 pass, and the step time.
 
   python tools/c3_diag.py [--n 125000000] [--d 64] [--k 1000] [--iters 10]
+                          [--resort-at IT]
+
+--resort-at IT: before iteration IT, rebuild the label-sorted image from the
+current labels (dkm_x_image_sorted, the buffer reused) and print its time:
+whether one re-sort pays back through cheaper screens.
 """
 import argparse
 import os
@@ -21,6 +26,7 @@ def main():
     p.add_argument("--d", type=int, default=64)
     p.add_argument("--k", type=int, default=1000)
     p.add_argument("--iters", type=int, default=10)
+    p.add_argument("--resort-at", type=int, default=-1)
     a = p.parse_args()
     import torch
     from dislib_amd import _device
@@ -39,6 +45,15 @@ def main():
     tile_b = (a.d + 15) // 16 * 1024
     prev_c = (0, 0, 0, 0)
     for it in range(a.iters):
+        if it == a.resort_at and st.simg is not None:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            with st._on():
+                st.simg = _device.sorted_image(st.dd, st.labels[:a.n], a.k,
+                                               st.ws, old=st.simg)
+            torch.cuda.synchronize()
+            print({"resort_ms": round((time.perf_counter() - t0) * 1e3, 2)},
+                  flush=True)
         before = st.labels[:a.n].clone()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
