@@ -57,7 +57,12 @@ constexpr size_t LDS_PER_CU = 160 * 1024;
 // Accumulation mode bits: AM_ON (accumulate at all), AM_DELTA (incremental:
 // only label changes move rows), AM_INLDS (block-private LDS accumulators,
 // flushed once per block; else fp64 global atomics).
-enum : int { AM_NONE = 0, AM_ON = 1, AM_DELTA = 2, AM_INLDS = 4 };
+// AM_MLIST (k_screen_w32, with AM_DELTA and without AM_ON): the rows the
+// screen moves are listed (v.smoved, count hdr->nmoved; previous labels in
+// v.queue[row]) for sorted_sums_moved instead of added in the screen.
+enum : int { AM_NONE = 0, AM_ON = 1, AM_DELTA = 2, AM_INLDS = 4,
+             AM_MLIST = 8 };
+constexpr int W32_MLB = 256;  // AM_MLIST: moved rows staged per wave (LDS)
 __host__ __device__ __forceinline__ bool am_full(int m) {
   return (m & (AM_ON | AM_DELTA)) == AM_ON;
 }
@@ -383,6 +388,10 @@ constexpr int SB = DKM_SB;  // screen block: SB/64 waves share one LDS image
 #ifndef DKM_AB_NO_W32
 #define DKM_AB_NO_W32 0
 #endif
+#ifndef DKM_AB_NO_MLIST
+#define DKM_AB_NO_MLIST 0
+#endif
+constexpr bool AB_NO_MLIST = DKM_AB_NO_MLIST;
 #ifndef DKM_AB_DELTA_POST
 #define DKM_AB_DELTA_POST 0
 #endif
@@ -1137,6 +1146,22 @@ __global__ void __launch_bounds__(SBW) __attribute__((
   int2 *wl = v.tlist + seg * TL_CAP;
   const bool listing = use_list && seg < TL_SEGS;
   int tl_cnt = 0, tl_over = 0;
+  // AM_MLIST: this wave's staged moved rows (after the scratch and the
+  // threshold norms), reserved in the global list W32_MLB at a time
+  const bool mlist = (amode & AM_MLIST) != 0;
+  int *mbuf = (int *)(scr0 + (IMG ? 0 : (SBW / 64) * W32_SCR) +
+                      (HINT ? kpad32(k) * 64 : 0)) +
+              wid * W32_MLB;
+  int mcnt = 0;  // wave-uniform
+  auto mflush = [&]() {
+    wave_sync_w();
+    int at0 = 0;
+    if (lane == 0) at0 = atomicAdd(&v.hdr->nmoved, mcnt);
+    at0 = __shfl(at0, 0, 64);
+    for (int e = lane; e < mcnt; e += 64) v.smoved[at0 + e] = mbuf[e];
+    wave_sync_w();
+    mcnt = 0;
+  };
 
   // Whole 128-B lines per wave-instruction (tools/membench.hip: loading
   // each lane's own 16 features touched 64 lines per instruction and
@@ -1486,7 +1511,7 @@ __global__ void __launch_bounds__(SBW) __attribute__((
       if (unique) {
         if (full_acc) {
           // added above
-        } else if (delta && lab != prev) {
+        } else if (delta && lab != prev && !mlist) {
           const TX *xr = X + si * ldx;
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
@@ -1506,8 +1531,23 @@ __global__ void __launch_bounds__(SBW) __attribute__((
         }
       }
     }
+    if (mlist) {
+      // a row the screen moved: listed with its previous label
+      const bool mv = h == 0 && si < n && unique && ri != prev;
+      const uint64_t mm = __ballot(mv);
+      if (mm) {
+        const int c = __popcll(mm);
+        if (mcnt + c > W32_MLB) mflush();
+        if (mv) {
+          mbuf[mcnt + lane_prefix(mm)] = (int)si;
+          v.queue[si] = prev;
+        }
+        mcnt += c;
+      }
+    }
     if (!IMG && full_acc && s_next < n) load_tile(s_next);
   }
+  if (mlist && mcnt) mflush();
   if (lane == 0) {
     if (listing) v.tcount[seg] = tl_cnt;
     if (tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
@@ -2702,6 +2742,71 @@ static int launch_screen_t(const TX *X, int64_t end, int d, int64_t ldx,
   return check_launch("screen assignment");
 }
 
+// The rows an AM_MLIST screen moved (v.smoved, *cnt of them; new label in
+// lab, previous in prevs[row]): +x to the new cluster, -x to the previous
+// one, into block-private LDS sums flushed once per block.  Lanes over
+// features (d <= 32: two rows per wave instruction), MV_U row pairs in
+// flight per wave; the list order is free, so no sort (the sorted segment
+// sums walked 4.7 M listed rows at 0.55 TB/s, 4.4 ms, at C2's iteration 2).
+constexpr int MV_U = 8;
+template <class TX>
+__global__ void __launch_bounds__(256)
+    k_moved_sums(const TX *__restrict__ X, int64_t ldx, int d,
+                 const int32_t *__restrict__ list, const int32_t *cnt,
+                 const int32_t *__restrict__ lab,
+                 const int32_t *__restrict__ prevs, int k, double *acc) {
+  extern __shared__ double lds_acc[];
+  zero_lds_acc(lds_acc, k, d);
+  __syncthreads();
+  const int ds = lds_stride(d);
+  const int lane = threadIdx.x & 63, g = lane >> 5, f = lane & 31;
+  const int64_t m = *cnt;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  for (int64_t p0 = w * 2 * MV_U; p0 < m; p0 += nw * 2 * MV_U) {
+    int64_t row[MV_U];
+#pragma unroll
+    for (int u = 0; u < MV_U; ++u) {
+      const int64_t p = p0 + 2 * u + g;
+      row[u] = p < m ? (int64_t)list[p] : -1;
+    }
+    int lb[MV_U], pv[MV_U];
+    double x[MV_U];
+#pragma unroll
+    for (int u = 0; u < MV_U; ++u) {
+      const bool ok = row[u] >= 0;
+      lb[u] = ok ? lab[row[u]] : -1;
+      pv[u] = ok ? prevs[row[u]] : -1;
+      x[u] = ok && f < d ? (double)X[row[u] * ldx + f] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < MV_U; ++u) {
+      if (lb[u] < 0) continue;
+      if (f < d) {
+        lds_add(lds_acc + (int64_t)lb[u] * ds + f, x[u]);
+        if (pv[u] >= 0) lds_add(lds_acc + (int64_t)pv[u] * ds + f, -x[u]);
+      }
+      if (f == 0) {
+        lds_add(lds_acc + (int64_t)k * ds + lb[u], 1.0);
+        if (pv[u] >= 0) lds_add(lds_acc + (int64_t)k * ds + pv[u], -1.0);
+      }
+    }
+  }
+  __syncthreads();
+  flush_lds_acc(lds_acc, acc, k, d);
+}
+
+template <class TX>
+static int launch_moved_sums(const TX *X, int64_t ldx, int d, int k,
+                             const int32_t *lab, double *acc, const WsView &v,
+                             hipStream_t s) {
+  const size_t lds = (size_t)lds_acc_len(k, d) * 8;
+  if (d > 32 || lds > 64 * 1024) return 1;
+  k_moved_sums<TX><<<(unsigned)dev_info().cus, 256, lds, s>>>(
+      X, ldx, d, v.smoved, &v.hdr->nmoved, lab, v.queue, k, acc);
+  return check_launch("moved-row sums");
+}
+
 template <class TX>
 static int launch_screen_w32(const TX *X, int64_t end, int d, int64_t ldx,
                              int k, const WsView &v, int32_t *lab_out,
@@ -2720,6 +2825,11 @@ static int launch_screen_w32(const TX *X, int64_t end, int d, int64_t ldx,
   const bool hint = im && (amode & AM_DELTA) && k <= W32_HINT_KMAX &&
                     lds + pcn_bytes <= LDS_BUDGET;
   if (hint) lds += pcn_bytes;
+  // AM_MLIST: the moved-row staging after them (the kernel's layout)
+  if (amode & AM_MLIST) {
+    if (!(im && hint)) return 1;  // the image threshold pass only
+    lds += (size_t)(SBW / 64) * W32_MLB * 4;
+  }
   const void *kf = hint ? (const void *)k_screen_w32<TX, true, true>
                    : im ? (const void *)k_screen_w32<TX, true>
                         : (const void *)k_screen_w32<TX, false>;
@@ -3314,6 +3424,15 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
         return r;
     }
   }
+  // the d <= 32 image threshold pass of a delta call: the rows it moves
+  // are listed and summed by sorted_sums_moved after the re-checks (a
+  // moved row's fp64 load and +-x adds inside the screen stalled its wave:
+  // C2's iteration 2, 4.7 % of the rows moving, took 7.2 ms against 3.7)
+  bool mlist = w32 && acc_kind == 2 && !post && labels && chunk >= n &&
+               img.tiles && img.kind == IMG_SPLIT && !build_img &&
+               (int64_t)n <= nq && sorted_sums_ok(k, n, v) && !AB_NO_MLIST;
+  if (mlist && hipMemsetAsync(&v.hdr->nmoved, 0, 4, s) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "screen: memset");
   for (int64_t base = 0; base < n; base += chunk) {
     const int64_t end = std::min(n, base + chunk);
     int32_t *lab_out = labels ? labels : v.queue - base;
@@ -3336,10 +3455,18 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
       r = launch_cand2<TX>(X, d, ldx, C, v, lab_out, base, nseg, s);
       if (!r && hint) r = launch_candn<TX>(X, d, ldx, C, v, lab_out, base,
                                            nseg, s);
-    } else if (w32)
-      r = launch_screen_w32<TX>(X, end, d, ldx, k, v, lab_out, acc, amode,
-                                base, lds, use_list, s, &nseg, img,
-                                fuse_build);
+    } else if (w32) {
+      r = mlist ? launch_screen_w32<TX>(X, end, d, ldx, k, v, lab_out, acc,
+                                        AM_DELTA | AM_MLIST, base, fb,
+                                        use_list, s, &nseg, img)
+                : 1;
+      if (r == 1) {
+        mlist = false;
+        r = launch_screen_w32<TX>(X, end, d, ldx, k, v, lab_out, acc, amode,
+                                  base, lds, use_list, s, &nseg, img,
+                                  fuse_build);
+      }
+    }
     else if (prec == P_F32)
       r = vec ? launch_screen_nks<P_F32, true, TX>(X, end, d, ldx, k, v,
                                                    lab_out, acc, amode, base,
@@ -3376,7 +3503,13 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
                                     premoved ? &v.hdr->nmoved : nullptr,
                                     premoved ? v.queue : nullptr)))
       return r;
-    if (premoved) {
+    if (mlist) {
+      r = launch_moved_sums<TX>(X, ldx, d, k, lab_out, acc, v, s);
+      if (r == 1)
+        r = sorted_sums_moved<TX>(X, n, d, ldx, lab_out, v.queue, k, acc, v,
+                                  s);
+      if (r) return r;
+    } else if (premoved) {
       if ((r = sorted_sums_moved<TX>(X, n, d, ldx, lab_out, v.queue, k, acc,
                                      v, s)))
         return r;
