@@ -43,37 +43,50 @@ __global__ void __launch_bounds__(CBLOCK)
     const int2 *list = v.clist + sg * B1_CAP + t0;
     const int m = min(64, cnt - t0);
     const int2 own = list[min(lane, m - 1)];  // the batch, one entry a lane
-    for (int p = 0; p < m; p += 8) {
-      const bool live = p + e < m;
-      const int src = min(p + e, m - 1);
-      const int sx = __shfl(own.x, src, 64), sy = __shfl(own.y, src, 64);
-      const int c1 = sy & 0xffff, c2 = (int)((unsigned)sy >> 16);
-      const int64_t si = base + sx;
-      const TX *xr = X + si * ldx + j;
-      const double *cr1 = C + (int64_t)c1 * d + j;
-      const double *cr2 = C + (int64_t)c2 * d + j;
-      double xv[NST], a[NST], b[NST];
+    // two 8-entry steps per pass, every load of both issued before the
+    // first use (one step in flight per wave read the rows at 0.31 of HBM)
+    for (int p = 0; p < m; p += 16) {
+      double xv[2][NST], a[2][NST], b[2][NST];
+      int64_t si[2];
+      int c1[2], c2[2];
+      bool live[2];
 #pragma unroll
-      for (int i = 0; i < NST; ++i) {
-        xv[i] = (double)xr[8 * i];
-        a[i] = cr1[8 * i];
-        b[i] = cr2[8 * i];
-      }
-      double r1 = 0.0, r2 = 0.0;
+      for (int h = 0; h < 2; ++h) {
+        live[h] = p + 8 * h + e < m;
+        const int src = min(p + 8 * h + e, m - 1);
+        const int sx = __shfl(own.x, src, 64), sy = __shfl(own.y, src, 64);
+        c1[h] = sy & 0xffff;
+        c2[h] = (int)((unsigned)sy >> 16);
+        si[h] = base + sx;
+        const TX *xr = X + si[h] * ldx + j;
+        const double *cr1 = C + (int64_t)c1[h] * d + j;
+        const double *cr2 = C + (int64_t)c2[h] * d + j;
 #pragma unroll
-      for (int i = 0; i < NST; ++i) {
-        const double d1 = xv[i] - a[i], d2 = xv[i] - b[i];
-        r1 = i ? r1 + d1 * d1 : d1 * d1;
-        r2 = i ? r2 + d2 * d2 : d2 * d2;
+        for (int i = 0; i < NST; ++i) {
+          xv[h][i] = (double)xr[8 * i];
+          a[h][i] = cr1[8 * i];
+          b[h][i] = cr2[8 * i];
+        }
       }
 #pragma unroll
-      for (int off = 1; off < 8; off <<= 1) {
-        r1 = r1 + __shfl_xor(r1, off, 64);
-        r2 = r2 + __shfl_xor(r2, off, 64);
+      for (int h = 0; h < 2; ++h) {
+        double r1 = 0.0, r2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < NST; ++i) {
+          const double d1 = xv[h][i] - a[h][i], d2 = xv[h][i] - b[h][i];
+          r1 = i ? r1 + d1 * d1 : d1 * d1;
+          r2 = i ? r2 + d2 * d2 : d2 * d2;
+        }
+#pragma unroll
+        for (int off = 1; off < 8; off <<= 1) {
+          r1 = r1 + __shfl_xor(r1, off, 64);
+          r2 = r2 + __shfl_xor(r2, off, 64);
+        }
+        const double q1 = argmin_key(sqrt(r1)), q2 = argmin_key(sqrt(r2));
+        if (live[h] && j == 0)
+          lab_out[si[h]] =
+              (q2 < q1 || (q2 == q1 && c2[h] < c1[h])) ? c2[h] : c1[h];
       }
-      const double q1 = argmin_key(sqrt(r1)), q2 = argmin_key(sqrt(r2));
-      if (live && j == 0)
-        lab_out[si] = (q2 < q1 || (q2 == q1 && c2 < c1)) ? c2 : c1;
     }
   }
   if (mine) atomicAdd((unsigned long long *)&v.hdr->rechecked_total, mine);
