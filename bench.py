@@ -512,12 +512,14 @@ def binding_for(d, k, csr_nnz):
                 "(profiles/r05/pmc/c4_pmc_summary_10M.txt)")
     if k * d > 32 * 128:
         return ("instruction issue of k_screen_sorted over the label-sorted "
-                "image: VALU:MFMA 7.4:1, 45% MFMA busy, SQ_WAIT_ANY 35% "
-                "(profiles/r05/pmc/c3_sorted_pmc_summary_20M_r05z.txt)")
+                "image: VALU:MFMA 7.4:1, SALU 6 per MFMA, SQ_WAIT_ANY 35% "
+                "and SQ_WAIT_INST_ANY 28% of wave cycles; 173 B/sample of "
+                "HBM traffic per steady iteration "
+                "(profiles/r06/pmc/c3_pmc_summary_20M.txt)")
     return ("instruction issue of k_screen_w32 over the split image: "
-            "VALU:MFMA 13.4:1, SQ_WAIT_ANY 35% at 3 waves per SIMD; the "
-            "image stream runs at about half of HBM "
-            "(profiles/r05/pmc/c2_pmc_summary_20M.txt)")
+            "VALU:MFMA 13.4:1, SQ_WAIT_ANY 47% of wave cycles; 143 "
+            "B/sample of HBM traffic per steady iteration, streamed at "
+            "about half of HBM (profiles/r06/pmc/c2_pmc_summary_20M.txt)")
 
 
 def main():
