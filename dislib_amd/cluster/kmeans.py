@@ -273,6 +273,15 @@ class _Lloyd:
                 mode = _lib.MODE_BF16X3
             if self.sorting:
                 image = (None, 0)
+            else:
+                # the image the later (auto) iterations stream: a d <= 32
+                # or GEMM-shaped bf16x3 pass writes it as it converts X
+                # (DKM_IMAGE_BUILD); other shapes take none here
+                image = self.dd.screen_image(self.k, _lib.MODE_AUTO)
+                if (image[0] is None or not image[1] & _lib.IMAGE_BUILD or
+                        image[1] & ~_lib.IMAGE_BUILD not in
+                        (_lib.IMAGE_SPLIT, _lib.IMAGE_GEMM)):
+                    image = None   # none, or built: this pass streams X
         elif self.sorting:
             if self.it <= SORT_AT:
                 # the labels of the initial centres are poor hints (most

@@ -388,6 +388,10 @@ constexpr int SB = DKM_SB;  // screen block: SB/64 waves share one LDS image
 #ifndef DKM_AB_NO_W32
 #define DKM_AB_NO_W32 0
 #endif
+#ifndef DKM_AB_NO_GEMM_BUILD
+#define DKM_AB_NO_GEMM_BUILD 0
+#endif
+constexpr bool AB_NO_GEMM_BUILD = DKM_AB_NO_GEMM_BUILD;
 #ifndef DKM_AB_NO_MLIST
 #define DKM_AB_NO_MLIST 0
 #endif
@@ -3530,11 +3534,14 @@ template <class TX>
 static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
                        const double *C, int k, const WsView &v, size_t wsb,
                        int32_t *labels, double *acc, int acc_kind,
-                       bool one, const XImage *img, hipStream_t s) {
+                       bool one, const XImage *img, hipStream_t s,
+                       const XImage *bimg = nullptr) {
   (void)wsb;
   const int64_t nq = std::min<int64_t>(v.nq, INT32_MAX);
   if (!labels && nq < 1)
     return fail(DKM_E_WORKSPACE, "gemm: no label scratch");
+  if (bimg && !labels)
+    return fail(DKM_E_ARG, "gemm: image build needs the labels");
   const int64_t chunk = labels ? n : nq;
   const bool post =
       acc_kind != 0 && (acc_kind == 1 || (labels && nq >= n));
@@ -3550,7 +3557,8 @@ static int launch_gemm(const TX *X, int64_t n, int d, int64_t ldx,
     const int64_t end = std::min(n, base + chunk);
     int32_t *lab_out = labels ? labels : v.queue - base;
     int r = gemm_screen<TX>(X, base, end, d, ldx, C, k, v, lab_out,
-                            skind ? acc : nullptr, skind == 2, one, img, s);
+                            skind ? acc : nullptr, skind == 2, one, img, s,
+                            bimg);
     if (r) return r;
     if (post && (r = launch_post_sums<TX>(X, base, end, d, ldx, lab_out,
                                           prevbuf, k, acc, v, s)))
@@ -3614,7 +3622,11 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
                                "screen (MODE_SCREEN_BF16 or AUTO) and labels");
   const bool split_w32 = image_kind == IMG_SPLIT && mode ==
       DKM_MODE_SCREEN_BF16X3 && screen_ok(k, d) && d <= 32;
-  if (build && !split_w32) {
+  // the bf16x3 GEMM screen's chunk splits write the single-product image's
+  // hi tiles as they convert X (the fit's first iteration; no image pass)
+  const bool split_gemm = build && image_kind == IMG_GEMM && labels &&
+      mode == DKM_MODE_SCREEN_BF16X3 && gemm_path(k, d) && !AB_NO_GEMM_BUILD;
+  if (build && !split_w32 && !split_gemm) {
     // no screen writes this kind in its pass: build it first
     if (int r = x_image<TX>(X, n, d, ldx, image_kind, (void *)image,
                             x_image_bytes(n, d, image_kind), stream, who))
@@ -3632,9 +3644,12 @@ static int assign(const TX *X, int64_t n, int64_t d, int64_t ldx,
     const bool use_img = image && image_kind == IMG_GEMM &&
                          mode == DKM_MODE_SCREEN_BF16;
     if (use_img) gimg = x_image_view(image, n, d, IMG_GEMM);
+    XImage bimg;
+    if (split_gemm) bimg = x_image_view(image, n, d, IMG_GEMM);
     return launch_gemm<TX>(X, n, (int)d, ldx, C, (int)k, v, wsb, labels, acc,
                            acc_kind, mode == DKM_MODE_SCREEN_BF16,
-                           use_img ? &gimg : nullptr, s);
+                           use_img ? &gimg : nullptr, s,
+                           split_gemm ? &bimg : nullptr);
   }
   if (mode == DKM_MODE_SCREEN32 || mode == DKM_MODE_SCREEN_BF16X3 ||
       mode == DKM_MODE_SCREEN_BF16) {

@@ -105,13 +105,16 @@ __device__ __forceinline__ void top_insert(float v, int i, float (&V)[GTOP],
 // into mrows/GT tiles; rows past nrows and features past d are zero.  One
 // wave = 8 rows, lane (row rr = l >> 3, group f = l & 7): 8 lanes read 512
 // contiguous bytes of a row per step.  xn (nullable): fp32 upper bound of
-// the row's Euclidean norm.
+// the row's Euclidean norm.  out1 / xn1 (hi + lo splits only, nullable): the
+// same rows' hi-only tiles and norms in the resident IMG_GEMM image as well
+// (DKM_IMAGE_BUILD during the bf16x3 iteration: no separate image pass).
 // ---------------------------------------------------------------------------
 template <bool VEC, class TX>
 __global__ void __launch_bounds__(256)
     k_gemm_split(const TX *__restrict__ X, int64_t row0, int64_t nrows,
                  int64_t mrows, int d, int64_t ldx, int nks, double scale,
-                 char *__restrict__ out, float *__restrict__ xn, int one) {
+                 char *__restrict__ out, float *__restrict__ xn, int one,
+                 char *__restrict__ out1, float *__restrict__ xn1) {
   const int lane = threadIdx.x & 63, rr = lane >> 3, f = lane & 7;
   const int64_t wv = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nw = (int64_t)gridDim.x * 4;
@@ -181,13 +184,20 @@ __global__ void __launch_bounds__(256)
             make_uint4(hw[0], hw[1], hw[2], hw[3]);
         *(uint4 *)(tile + 16 * gslot(r, 4 + c)) =
             make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        if (out1) {
+          char *t1 = out1 + (st * nks + ks) * (int64_t)GSTAGE1 + r * 64;
+          *(uint4 *)(t1 + 16 * gslot1(r, c)) =
+              make_uint4(hw[0], hw[1], hw[2], hw[3]);
+        }
       }
     }
     ss += __shfl_xor(ss, 1, 64);
     ss += __shfl_xor(ss, 2, 64);
     ss += __shfl_xor(ss, 4, 64);
     // fl32 of sqrt may round down by 2^-24: inflate (NaN / Inf stay so)
-    if (xn && f == 0) xn[row] = valid ? (float)sqrt(ss) * (1.0f + 0x1.0p-20f) : 0.0f;
+    const float nr = valid ? (float)sqrt(ss) * (1.0f + 0x1.0p-20f) : 0.0f;
+    if (xn && f == 0) xn[row] = nr;
+    if (xn1 && f == 0) xn1[row] = nr;
   }
 }
 
@@ -1041,17 +1051,18 @@ __global__ void __launch_bounds__(1024)
 template <class TX>
 int launch_split(const TX *X, int64_t row0, int64_t nrows, int64_t mrows,
                  int d, int64_t ldx, double scale, char *out, float *xn,
-                 int one, hipStream_t s) {
+                 int one, hipStream_t s, char *out1 = nullptr,
+                 float *xn1 = nullptr) {
   const int nks = (int)(dpad32(d) / GBK);
   const bool vec = (d % 8 == 0) && ((ldx * (int64_t)sizeof(TX)) % 16 == 0) &&
                    ((uintptr_t)X % 16 == 0);
   const int64_t blocks = std::min<int64_t>((mrows + 31) / 32, 16384);
   if (vec)
     k_gemm_split<true, TX><<<(unsigned)blocks, 256, 0, s>>>(
-        X, row0, nrows, mrows, d, ldx, nks, scale, out, xn, one);
+        X, row0, nrows, mrows, d, ldx, nks, scale, out, xn, one, out1, xn1);
   else
     k_gemm_split<false, TX><<<(unsigned)blocks, 256, 0, s>>>(
-        X, row0, nrows, mrows, d, ldx, nks, scale, out, xn, one);
+        X, row0, nrows, mrows, d, ldx, nks, scale, out, xn, one, out1, xn1);
   return check_launch("gemm split");
 }
 
@@ -1107,8 +1118,13 @@ template <class TX>
 int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
                 const double *C, int k, const WsView &v, int32_t *lab_out,
                 double *acc, bool delta, bool one, const XImage *img,
-                hipStream_t s) {
+                hipStream_t s, const XImage *bimg) {
   if (!v.gfrag) return fail(DKM_E_WORKSPACE, "gemm_screen: no GEMM region");
+  // bimg: the IMG_GEMM image the bf16x3 splits also write (whole tiles from
+  // row 0 of the image)
+  if (bimg && (one || base % GT || v.gchunk % GT))
+    return fail(DKM_E_ARG, "gemm_screen: image build needs the bf16x3 "
+                           "splits on whole tiles");
   const void *kf = one ? (const void *)k_gemm_screen1
                        : (const void *)k_gemm_screen3;
   if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1140,8 +1156,12 @@ int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
     const int64_t rows = std::min<int64_t>(v.gchunk, end - c0);
     if (hipStreamWaitEvent(ss.s, ss.free_ev[b], 0) != hipSuccess)
       return fail(DKM_E_LAUNCH, "gemm: stream wait");
-    if (int r = launch_split<TX>(X, c0, rows, round_up(rows, GT), d, ldx, 1.0,
-                                 xs_b[b], xn_b[b], one ? 1 : 0, ss.s))
+    if (int r = launch_split<TX>(
+            X, c0, rows, round_up(rows, GT), d, ldx, 1.0, xs_b[b], xn_b[b],
+            one ? 1 : 0, ss.s,
+            bimg ? (char *)bimg->tiles + (c0 / GT) * (int64_t)nks * GSTAGE1
+                 : nullptr,
+            bimg ? (float *)bimg->xx + c0 : nullptr))
       return r;
     if (hipEventRecord(ss.split_ev[b], ss.s) != hipSuccess)
       return fail(DKM_E_LAUNCH, "gemm: event");
@@ -1230,11 +1250,11 @@ int gemm_image(const TX *X, int64_t n, int d, int64_t ldx, const XImage &img,
 template int gemm_screen<double>(const double *, int64_t, int64_t, int,
                                  int64_t, const double *, int, const WsView &,
                                  int32_t *, double *, bool, bool,
-                                 const XImage *, hipStream_t);
+                                 const XImage *, hipStream_t, const XImage *);
 template int gemm_screen<float>(const float *, int64_t, int64_t, int, int64_t,
                                 const double *, int, const WsView &,
                                 int32_t *, double *, bool, bool,
-                                const XImage *, hipStream_t);
+                                const XImage *, hipStream_t, const XImage *);
 template int gemm_image<double>(const double *, int64_t, int, int64_t,
                                 const XImage &, hipStream_t);
 template int gemm_image<float>(const float *, int64_t, int, int64_t,

@@ -546,12 +546,13 @@ int gemm_prepare(const double *C, int64_t k, int64_t d, const WsView &v,
 // counted in hdr->qcount).  acc != NULL: the merge step also moves rows
 // between the sums with fp64 atomics (delta = true: only changed labels).
 // img (IMG_GEMM, or NULL): the resident sample tiles the single-product
-// screen reads instead of splitting X (chunks starting on a 256-row tile)
+// screen reads instead of splitting X (chunks starting on a 256-row tile).
+// bimg (bf16x3 only, or NULL): the IMG_GEMM image the chunk splits write too.
 template <class TX>
 int gemm_screen(const TX *X, int64_t base, int64_t end, int d, int64_t ldx,
                 const double *C, int k, const WsView &v, int32_t *lab_out,
                 double *acc, bool delta, bool one, const XImage *img,
-                hipStream_t s);
+                hipStream_t s, const XImage *bimg = nullptr);
 // the IMG_GEMM image of X (x_image_view layout)
 template <class TX>
 int gemm_image(const TX *X, int64_t n, int d, int64_t ldx, const XImage &img,

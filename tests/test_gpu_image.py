@@ -168,3 +168,56 @@ def test_full_sums_pass_builds_the_split_image(n, d, k, f32):
     _device.assign_delta(dd, Ct2, ws, lab, acc, mode)
     rl2, _, _ = orc.partial_sum(x, C2)
     assert np.array_equal(lab.cpu().numpy(), rl2)
+
+
+@pytest.mark.parametrize("n,d,k,f32", [(150001, 160, 300, False),
+                                       (70000, 200, 129, True)])
+def test_bf16x3_gemm_pass_builds_the_gemm_image(n, d, k, f32):
+    """DKM_IMAGE_BUILD on the GEMM shapes (round 6): the bf16x3 iteration's
+    chunk splits also write the single-product image (hi tiles + norms) of
+    every chunk, byte for byte what dkm_x_image_* builds in its own pass;
+    the call's labels and sums are the oracle's, and a single-product delta
+    launch through the fused image matches the oracle too."""
+    from dislib_amd import _device, _lib
+    from dislib_amd.data import load_data
+    so = _lib.lib()
+    rng = np.random.default_rng(n + d + k)
+    blobs = rng.uniform(-10, 10, (k, d))
+    x = blobs[rng.integers(0, k, n)] + rng.standard_normal((n, d))
+    if f32:
+        x = x.astype(np.float32)
+    C = blobs + 0.3 * rng.standard_normal((k, d))
+    dev = torch.device("cuda", 0)
+    dd = load_data(x, subset_size=n)._device_data()
+    ws = _device.Workspace(k, d, n, dev)
+    acc = torch.zeros(k * (d + 1), dtype=torch.float64, device=dev)
+    Ct = torch.from_numpy(C).to(dev)
+    lab = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    _device.prepare(Ct, ws, acc)
+    img, kind = dd.screen_image(k, _lib.MODE_AUTO)
+    assert kind == _lib.IMAGE_GEMM | _lib.IMAGE_BUILD
+    img.fill_(0xAB)
+    _device.partial_sum(dd, Ct, ws, lab, acc, _lib.MODE_BF16X3,
+                        image=(img, kind))
+    assert not dd._unbuilt
+    rl, rs, rc = orc.partial_sum(x, C)
+    assert np.array_equal(lab.cpu().numpy(), rl)
+    a = acc.cpu().numpy()
+    assert np.array_equal(a[k * d:], rc.astype(np.float64))
+    err = np.max(np.abs(a[:k * d].reshape(k, d) - rs) /
+                 np.maximum(np.abs(rs), 1.0))
+    assert err <= (1e-4 if f32 else 1e-11)
+    nb = so.dkm_x_image_bytes(n, d, _lib.IMAGE_GEMM)
+    ref = torch.full((img.numel(),), 0xAB, dtype=torch.uint8, device=dev)
+    fn = so.dkm_x_image_f32 if f32 else so.dkm_x_image_f64
+    _lib.check(fn(_device.ptr(dd.X), n, d, d, _lib.IMAGE_GEMM,
+                  _device.ptr(ref), nb, _device.stream_ptr()), "image")
+    assert torch.equal(img, ref)
+    # a single-product delta launch through the fused image
+    C2 = C + 0.2 * rng.standard_normal(C.shape)
+    Ct2 = torch.from_numpy(C2).to(dev)
+    acc.zero_()
+    _device.prepare(Ct2, ws, acc)
+    _device.assign_delta(dd, Ct2, ws, lab, acc, _lib.MODE_AUTO)
+    rl2, _, _ = orc.partial_sum(x, C2)
+    assert np.array_equal(lab.cpu().numpy(), rl2)

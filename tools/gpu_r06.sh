@@ -8,7 +8,7 @@
 #   bench     default bench.py (CPU baselines included)
 #   prof      rocprofv3 --kernel-trace --stats of bench.py --no-cpu
 #   c3it/c2it/c4it  one config's bench line under a kernel trace, per iteration
-#   c3ab/c2ab one config, main vs libdkm_$AB.so, two rounds
+#   c3ab/c2ab/c4ab one config, main vs libdkm_$AB.so, two rounds
 TAG=${1:-r06}; shift
 OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
 step() {  # name limit cmd...
@@ -66,7 +66,7 @@ for s in "$@"; do
     c3it) trace c3it 300 $C3 ;;
     c2it) trace c2it 300 $C2 ;;
     c4it) trace c4it 400 $C4 ;;
-    c3ab|c2ab) CMD=$C3; [ $s = c2ab ] && CMD=$C2
+    c3ab|c2ab|c4ab) CMD=$C3; [ $s = c2ab ] && CMD=$C2; [ $s = c4ab ] && CMD=$C4
       for r in 1 2; do for v in main ${AB:-ab}; do
         if [ $v = main ]; then unset DKM_LIB; else export DKM_LIB=$PWD/dislib_amd/libdkm_$v.so; fi
         step ${s}_$v$r 300 $CMD; summ $OUT/${TAG}_${s}_$v$r.log
