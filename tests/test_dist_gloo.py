@@ -1,4 +1,4 @@
-"""Multi-process (world_size 2 and 4, gloo, CPU) tests of the N>1 path's host
+"""Multi-process (world_size 2, 4 and 8, gloo, CPU) tests of the N>1 path's host
 logic: Subset sharding, the packed [sums | counts] all-reduce that replaces
 the reference's `_merge` arity tree (cluster/kmeans/base.py:137-143), the
 init-centre broadcast, and replicated convergence decisions.  The per-rank
@@ -210,15 +210,29 @@ def test_world4_ragged_and_empty_shards(sizes):
     """World size 4: ragged Subsets and ranks without rows (which still join
     every all-reduce) give the single-process result: identical centres
     and n_iter on every rank, every row labelled once, the oracle's fit."""
+    _check_ragged(sizes, 4)
+
+
+@pytest.mark.parametrize("sizes", [
+    [700, 1300, 50, 2100, 900, 1, 1600, 350, 10, 20, 3000],  # 1-2 per rank
+    [3000, 2500, 4000, 5],                        # four empty ranks
+])
+def test_world8_ragged_and_empty_shards(sizes):
+    """World size 8 (the driver's largest scaling run, rehearsed on gloo):
+    the same checks as world 4."""
+    _check_ragged(sizes, 8)
+
+
+def _check_ragged(sizes, world):
     from sklearn.datasets import make_blobs
     from oracle import kmeans_oracle as orc
-    res = _run(functools.partial(_lloyd_sizes, sizes=sizes), world=4)
+    res = _run(functools.partial(_lloyd_sizes, sizes=sizes), world=world)
     c0, i0, _, _ = res[0]
-    for r in range(4):
+    for r in range(world):
         assert np.array_equal(res[r][0], c0) and res[r][1] == i0
-    assert sum(res[r][2] for r in range(4)) == sum(sizes)
-    if len(sizes) < 4:
-        assert res[0][2] == 0
+    assert sum(res[r][2] for r in range(world)) == sum(sizes)
+    if len(sizes) < world:
+        assert sum(res[r][2] == 0 for r in range(world)) >= world - len(sizes)
     x, _ = make_blobs(n_samples=sum(sizes), n_features=5, centers=4,
                       random_state=7)
     edges = np.concatenate([[0], np.cumsum(sizes)])
@@ -227,5 +241,5 @@ def test_world4_ragged_and_empty_shards(sizes):
                  set_labels=True)
     assert i0 == ref.n_iter
     np.testing.assert_allclose(c0, ref.centers, rtol=1e-12, atol=1e-12)
-    lab = np.concatenate([res[r][3] for r in range(4)])
+    lab = np.concatenate([res[r][3] for r in range(world)])
     assert np.array_equal(lab, rl)
