@@ -802,11 +802,31 @@ __device__ double wave_sqdist(const TX *__restrict__ x,
     const int ci = base + lane, l = ci >> 3, j = ci & 7;
     if (l < t.n) {  // uniform over each 8-lane group
       const int lo = t.lo[l], len = t.len[l], full = len & ~7;
-      double df = (double)x[lo + j] - c[lo + j];
-      double r = df * df;
-      for (int i = 8; i < full; i += 8) {
-        df = (double)x[lo + i + j] - c[lo + i + j];
-        r = r + df * df;
+      double df, r;
+      if (len == 128) {
+        // numpy's full 128-element leaf: every load issued before the
+        // first add (the loop form waited one L2 / MALL round trip per 8
+        // elements of the centre row); the same additions in the same order
+        double xv[16], cv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          xv[u] = (double)x[lo + 8 * u + j];
+          cv[u] = c[lo + 8 * u + j];
+        }
+        df = xv[0] - cv[0];
+        r = df * df;
+#pragma unroll
+        for (int u = 1; u < 16; ++u) {
+          df = xv[u] - cv[u];
+          r = r + df * df;
+        }
+      } else {
+        df = (double)x[lo + j] - c[lo + j];
+        r = df * df;
+        for (int i = 8; i < full; i += 8) {
+          df = (double)x[lo + i + j] - c[lo + i + j];
+          r = r + df * df;
+        }
       }
       r = r + __shfl_xor(r, 1, 64);
       r = r + __shfl_xor(r, 2, 64);
