@@ -388,6 +388,10 @@ constexpr int SB = DKM_SB;  // screen block: SB/64 waves share one LDS image
 #ifndef DKM_AB_NO_W32
 #define DKM_AB_NO_W32 0
 #endif
+#ifndef DKM_AB_NO_C32
+#define DKM_AB_NO_C32 0
+#endif
+constexpr bool AB_NO_C32 = DKM_AB_NO_C32;
 #ifndef DKM_AB_NO_GEMM_BUILD
 #define DKM_AB_NO_GEMM_BUILD 0
 #endif
@@ -1560,6 +1564,250 @@ __global__ void __launch_bounds__(SBW) __attribute__((
     __syncthreads();
     flush_lds_acc(lds_acc, acc, k, d);
   }
+}
+
+// ---------------------------------------------------------------------------
+// The chunked bf16x3 screen on v_mfma_f32_32x32x16_bf16 (k_screen_c32):
+// labels-only launches with k x d fragments beyond LDS and 32 < d <= 64
+// (C3's first assignment, against the crowded initial centres).  k_screen's
+// 16x16x32 form read each fragment for 16 samples; this one reads it for 32
+// -- half the MFMA and LDS instructions per score and half the L2 -> LDS
+// fragment traffic per sample -- with the per-score work unchanged (the
+// packed top-2 of k_screen_w32's non-hinted pass).  Centres on the A rows in
+// b1frag's order (block cb, K-step ks: lane (r, h) holds -2c[32cb + r][16ks
+// + 8h + j], hi in b1frag, lo in b1frag_lo), staged through LDS in chunks of
+// C32_CB blocks; lane (r, h) of a wave holds sample r's features 16ks + 8h +
+// j as the B operand, converted from its fp64 row at the step's start (a
+// prefetched row cost 64 VGPRs: 2 waves per SIMD).  Output as k_screen's: labels, or
+// -(prev + 2) and the wave's undecided list.
+constexpr int SB32C = 512;  // 8 waves share each LDS chunk
+template <int NK>
+constexpr int c32_cb() {  // 32-centre blocks per chunk within LDS_BUDGET
+  return (int)(LDS_BUDGET / (NK * 2048 + 128));
+}
+template <class TX, int NK>
+__global__ void __launch_bounds__(SB32C) __attribute__((amdgpu_waves_per_eu(4)))
+    k_screen_c32(const TX *__restrict__ X, int64_t n, int d, int64_t ldx,
+                 int k, WsView v, int32_t *__restrict__ lab_out, int64_t base,
+                 int use_list) {
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  constexpr int CB = c32_cb<NK>();
+  constexpr int GB = 8;  // 32-centre blocks per packing group (128 tags)
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  char *frag = (char *)smem;                           // CB x NK x 2 KB
+  float *cnl = (float *)(frag + (int64_t)CB * NK * 2048);  // CB x 32
+  const int nkb = (int)(kpad32(k) / 32);
+  const float cm =
+      (float)__longlong_as_double((long long)v.hdr->cmax_bits) * 1.000001f;
+  const BoundK bk = bound_consts<P_B3>(d, cm);
+  const float ninf = __uint_as_float(opaque_u32(0xff800000u));
+  const uint32_t vmask = opaque_u32(~PACK_MASK);
+  const int lane = threadIdx.x & 63, h = lane >> 5, r = lane & 31;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t seg = (int64_t)blockIdx.x * (SB32C / 64) + wid;
+  const int64_t step = (int64_t)gridDim.x * (SB32C / 64) * 32;
+  int2 *wl = v.tlist + seg * TL_CAP;
+  const bool listing = use_list && seg < TL_SEGS;
+  int tl_cnt = 0, tl_over = 0;
+  // LDS <- blocks [c0, c1): hi then lo fragments per (block, K-step), and
+  // the blocks' norms in accumulator order
+  auto load_chunk = [&](int c0, int c1) {
+    const f32x4 *hs = (const f32x4 *)(v.b1frag + (int64_t)c0 * NK * 512);
+    const f32x4 *ls = (const f32x4 *)(v.b1frag_lo + (int64_t)c0 * NK * 512);
+    f32x4 *dst = (f32x4 *)frag;
+    for (int e = threadIdx.x; e < (c1 - c0) * NK * 64; e += SB32C) {
+      const int blk = e >> 6, w = e & 63;
+      dst[blk * 128 + w] = hs[e];
+      dst[blk * 128 + 64 + w] = ls[e];
+    }
+    for (int e = threadIdx.x; e < (c1 - c0) * 32; e += SB32C)
+      cnl[e] = v.cn32f[c0 * 32 + e];
+  };
+  // this lane's piece of its sample's row: features 16ks + 8h + j
+  double raw[NK][8];
+  auto load_row = [&](int64_t s0) {
+    const int64_t si = s0 + r;
+    const bool ok = si < n;
+    const TX *xr = X + (ok ? si : 0) * ldx;
+#pragma unroll
+    for (int ks = 0; ks < NK; ++ks) {
+      const int t0 = 16 * ks + 8 * h;
+      if (ok && t0 + 8 <= d) {
+        if constexpr (sizeof(TX) == 8) {
+          const double2 *p = (const double2 *)(xr + t0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const double2 u = p[q];
+            raw[ks][2 * q] = u.x;
+            raw[ks][2 * q + 1] = u.y;
+          }
+        } else {
+          const float4 *p = (const float4 *)(xr + t0);
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const float4 u = p[q];
+            raw[ks][4 * q] = u.x;
+            raw[ks][4 * q + 1] = u.y;
+            raw[ks][4 * q + 2] = u.z;
+            raw[ks][4 * q + 3] = u.w;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) raw[ks][j] = 0.0;
+      }
+    }
+  };
+  // the block-uniform step loop (every wave reaches the chunk barriers)
+  const int64_t wofs = (int64_t)wid * 32;
+  int64_t s0 = base + seg * 32;
+  for (; s0 - wofs < n; s0 += step) {
+    load_row(s0);
+    bf16x8 xh[NK], xl[NK];
+    float xx = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NK; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const float x0 = (float)raw[ks][j], x1 = (float)raw[ks][j + 1];
+        xx = fmaf(x0, x0, xx);
+        xx = fmaf(x1, x1, xx);
+        const bf16x2 h2 = __builtin_convertvector(f32x2{x0, x1}, bf16x2);
+        const uint32_t hu = __builtin_bit_cast(uint32_t, h2);
+        const bf16x2 l2 = __builtin_convertvector(
+            f32x2{x0 - __uint_as_float(hu << 16),
+                  x1 - __uint_as_float(hu & 0xffff0000u)},
+            bf16x2);
+        xh[ks][j] = h2[0];
+        xh[ks][j + 1] = h2[1];
+        xl[ks][j] = l2[0];
+        xl[ks][j + 1] = l2[1];
+      }
+    {
+      float xa, xb;
+      pair_xor<32>(xx, xa, xb);
+      xx = xa + xb;
+    }
+    float r1 = INFINITY, r2 = INFINITY;
+    int ri = 0;
+    int cbase = 0;
+    auto chain = [&](int cb, f32x16 &accv) {
+      const f32x4 *c4p = (const f32x4 *)(cnl + (cb - cbase) * 32 + 16 * h);
+      const f32x4 c0 = c4p[0], c1 = c4p[1], c2 = c4p[2], c3 = c4p[3];
+      accv = f32x16{c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                    c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+#pragma unroll
+      for (int ks = 0; ks < NK; ++ks) {
+        const char *blk = frag + ((int64_t)(cb - cbase) * NK + ks) * 2048;
+        const bf16x8 ah = *(const bf16x8 *)(blk + lane * 16);
+        const bf16x8 al = *(const bf16x8 *)(blk + 1024 + lane * 16);
+        accv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xh[ks], accv, 0, 0,
+                                                       0);
+        accv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xl[ks], accv, 0, 0,
+                                                       0);
+        accv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, xh[ks], accv, 0, 0,
+                                                       0);
+      }
+    };
+    for (int c0 = 0; c0 < nkb; c0 += CB) {
+      const int c1 = min(nkb, c0 + CB);
+      __syncthreads();  // every wave is done with the previous chunk
+      load_chunk(c0, c1);
+      __syncthreads();
+      cbase = c0;
+      for (int g0 = c0; g0 < c1; g0 += GB) {
+        const int g1 = min(c1, g0 + GB);
+        float b1 = INFINITY, b2 = INFINITY;
+        auto score = [&](int cb, const f32x16 &accv) {
+          const uint32_t t0 = opaque_s32((uint32_t)((cb - g0) * 16));
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const float sp = __uint_as_float(
+                (__float_as_uint(accv[g]) & vmask) | (t0 + g));
+            b2 = __builtin_amdgcn_fmed3f(b1, b2, sp);
+            b1 = min_nc(b1, sp, ninf);
+          }
+        };
+        f32x16 acc_a, acc_b;
+        chain(g0, acc_a);
+        int cb = g0;
+        for (; cb + 2 <= g1; cb += 2) {
+          chain(cb + 1, acc_b);
+          score(cb, acc_a);
+          if (cb + 2 < g1) chain(cb + 2, acc_a);
+          score(cb + 1, acc_b);
+        }
+        if (cb < g1) score(cb, acc_a);
+        const uint32_t tg = __float_as_uint(b1) & PACK_MASK;
+        const int g = (int)(tg & 15);
+        const int gi =
+            (g0 + (int)(tg >> 4)) * 32 + (g & 3) + 8 * (g >> 2) + 4 * h;
+        const bool nw = b1 < r1;
+        r2 = nw ? min_nc(r1, b2, ninf) : min_nc(r2, b1, ninf);
+        ri = nw ? gi : ri;
+        r1 = nw ? b1 : r1;
+      }
+    }
+    {  // merge the two lanes of a sample (symmetric in the pair)
+      float a1, c1, a2, c2;
+      int ai, ci;
+      pair_xor<32>(r1, a1, c1);
+      pair_xor<32>(r2, a2, c2);
+      pair_xor<32>(ri, ai, ci);
+      const bool tc = (c1 < a1) | ((c1 == a1) & (ci < ai));
+      r1 = tc ? c1 : a1;
+      ri = tc ? ci : ai;
+      r2 = tc ? min_nc(a1, c2, ninf) : min_nc(a2, c1, ninf);
+    }
+    float xn;
+    const float B2 = bound2_fast(bk, xx, xn);
+    const int64_t si = s0 + r;
+    const bool sane = (xn < 1e18f) & (xn * cm < 1e30f) & (r1 < 1e30f);
+    const bool unique = sane & (r2 - r1 > B2);
+    const bool und = si < n && !unique;
+    const uint64_t um = __ballot(h == 0 && und);
+    const int add = __popcll(um);
+    if (listing && tl_cnt + add <= TL_CAP) {
+      if (h == 0 && und)
+        wl[tl_cnt + lane_prefix(um)] = make_int2((int)(si - base), -1);
+      tl_cnt += add;
+    } else {
+      tl_over += add;
+    }
+    if (h == 0 && si < n) lab_out[si] = unique ? ri : -1;
+  }
+  if (lane == 0) {
+    if (listing) v.tcount[seg] = tl_cnt;
+    if (tl_over) atomicAdd(&v.hdr->qcount, (uint32_t)tl_over);
+  }
+}
+
+template <class TX>
+static int launch_screen_c32(const TX *X, int64_t end, int d, int64_t ldx,
+                             int k, const WsView &v, int32_t *lab_out,
+                             int64_t base, int use_list, hipStream_t s,
+                             int *nseg) {
+  const int nk = (int)(dpad16(d) / 16);
+  if (!v.b1frag || !v.b1frag_lo || nk < 3 || nk > 4) return 1;
+  const void *kf = nk == 3 ? (const void *)k_screen_c32<TX, 3>
+                           : (const void *)k_screen_c32<TX, 4>;
+  const size_t lds = nk == 3 ? (size_t)c32_cb<3>() * (3 * 2048 + 128)
+                             : (size_t)c32_cb<4>() * (4 * 2048 + 128);
+  if (hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return fail(DKM_E_LAUNCH, "screen_c32: LDS attribute");
+  const int64_t cap = (int64_t)dev_info().cus * resident_blocks(kf, SB32C, lds);
+  const int64_t per_block = 32 * (SB32C / 64);
+  const int64_t need = (end - base + per_block - 1) / per_block;
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min(need, cap));
+  *nseg = (int)std::min<int64_t>((int64_t)g * (SB32C / 64), TL_SEGS);
+  if (nk == 3)
+    k_screen_c32<TX, 3><<<g, SB32C, lds, s>>>(X, end, d, ldx, k, v, lab_out,
+                                              base, use_list);
+  else
+    k_screen_c32<TX, 4><<<g, SB32C, lds, s>>>(X, end, d, ldx, k, v, lab_out,
+                                              base, use_list);
+  return check_launch("screen assignment (chunked 32x32)");
 }
 
 // ---------------------------------------------------------------------------
@@ -3478,14 +3726,22 @@ static int launch_screen(int prec, const TX *X, int64_t n, int d,
               : launch_screen_nks<P_F32, false, TX>(X, end, d, ldx, k, v,
                                                     lab_out, acc, amode, base,
                                                     lds, use_list, chb, s, &nseg);
-    else
-      r = vec ? launch_screen_nks<P_B3, true, TX>(X, end, d, ldx, k, v,
-                                                  lab_out, acc, amode, base,
-                                                  lds, use_list | (c2 ? 2 : 0),
-                                                  chb, s, &nseg)
-              : launch_screen_nks<P_B3, false, TX>(X, end, d, ldx, k, v,
-                                                   lab_out, acc, amode, base,
-                                                   lds, use_list, chb, s, &nseg);
+    else {
+      // the chunked labels-only bf16x3 screen in 32x32x16 form (32 < d <= 64)
+      const bool c32 = chb && vec && amode == AM_NONE && !sub && d > 32 &&
+                       d <= 64 && !AB_NO_C32;
+      r = c32 ? launch_screen_c32<TX>(X, end, d, ldx, k, v, lab_out, base,
+                                      use_list, s, &nseg)
+              : 1;
+      if (r == 1)
+        r = vec ? launch_screen_nks<P_B3, true, TX>(
+                      X, end, d, ldx, k, v, lab_out, acc, amode, base, lds,
+                      use_list | (c2 ? 2 : 0), chb, s, &nseg)
+                : launch_screen_nks<P_B3, false, TX>(X, end, d, ldx, k, v,
+                                                     lab_out, acc, amode,
+                                                     base, lds, use_list, chb,
+                                                     s, &nseg);
+    }
     if (r) return r;
     if (c2 && (r = launch_cand2<TX>(X, d, ldx, C, v, lab_out, base,
                                     std::min(nseg, B1_SEGS), s)))

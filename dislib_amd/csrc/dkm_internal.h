@@ -79,7 +79,7 @@ struct WsHeader {
   uint64_t sfall_total;
   uint64_t umax_bits;  // max_c ||c - m||_2 (m: b1frag_t's translation)
 };
-constexpr uint64_t WS_MAGIC = 0x444b4d5753303034ull;  // "DKMWS004"
+constexpr uint64_t WS_MAGIC = 0x444b4d5753303035ull;  // "DKMWS005"
 constexpr size_t WS_HDR = 256;
 static_assert(sizeof(WsHeader) <= WS_HDR, "the header fits WS_HDR");
 
@@ -168,6 +168,9 @@ struct WsView {
   // b1_ok: b1frag of the translated centres -2 (c - m), m = mvec (fp32, the
   // centres' mean per feature; DKM_MODE_TRANSLATE)
   uint16_t *b1frag_t;
+  // b1_ok: the bf16 low parts of -2c in b1frag's order (hi = b1frag): the
+  // chunked bf16x3 screen in 32x32x16 form (k_screen_c32)
+  uint16_t *b1frag_lo;
   float *mvec;
   float *cn32f;   // kpad32 ||c||^2 in 32x32 accumulator order
   uint16_t *b1frag; // b1_ok: bf16 hi of -2c, 32x32x16 order, dpad16 / 16

@@ -69,6 +69,7 @@ size_t ws_bytes(int64_t k, int64_t d, int64_t n_queue) {
   if (b1_ok(k, d)) {
     b += round_up(kpad32(k) * dpad16(d) * 2, 256);  // b1frag
     b += round_up(kpad32(k) * dpad16(d) * 2, 256);  // b1frag_t
+    b += round_up(kpad32(k) * dpad16(d) * 2, 256);  // b1frag_lo
     b += round_up(d * 4, 256);                      // mvec
     b += (size_t)B1_SEGS * B1_CAP * 8;              // clist
     b += (size_t)B1_SEGS * 4;                       // ccount
@@ -132,6 +133,7 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
   v->gchunk = 0;
   v->b1frag = nullptr;
   v->b1frag_t = nullptr;
+  v->b1frag_lo = nullptr;
   v->mvec = nullptr;
   v->clist = nullptr;
   v->ccount = nullptr;
@@ -161,6 +163,8 @@ int ws_view(const void *ws, size_t bytes, int64_t k, int64_t d, WsView *v) {
     v->b1frag = (uint16_t *)p;
     p += round_up(kpad32(k) * dpad16(d) * 2, 256);
     v->b1frag_t = (uint16_t *)p;
+    p += round_up(kpad32(k) * dpad16(d) * 2, 256);
+    v->b1frag_lo = (uint16_t *)p;
     p += round_up(kpad32(k) * dpad16(d) * 2, 256);
     v->mvec = (float *)p;
     p += round_up(d * 4, 256);
@@ -376,8 +380,11 @@ __global__ void __launch_bounds__(256) k_frag(const double *__restrict__ C,
       const int64_t c = cb * 32 + (l & 31);
       const int64_t t = 16 * ks + 8 * (l >> 5) + j;
       const double x = (c < k && t < d) ? -2.0 * C[c * d + t] : 0.0;
-      v.b1frag[blk * 512 + l * 8 + j] =
-          __builtin_bit_cast(uint16_t, (__bf16)(float)x);
+      const __bf16 hi = (__bf16)(float)x;
+      v.b1frag[blk * 512 + l * 8 + j] = __builtin_bit_cast(uint16_t, hi);
+      // the bf16x3 low part in the same order (k_screen_c32)
+      v.b1frag_lo[blk * 512 + l * 8 + j] = __builtin_bit_cast(
+          uint16_t, (__bf16)(float)(x - (double)(float)hi));
       // the translated centres: -2 (c - m) rounded the same way
       const double xt =
           (c < k && t < d) ? -2.0 * (C[c * d + t] - (double)v.mvec[t]) : 0.0;
