@@ -1581,9 +1581,13 @@ __global__ void __launch_bounds__(SBW) __attribute__((
 // prefetched row cost 64 VGPRs: 2 waves per SIMD).  Output as k_screen's: labels, or
 // -(prev + 2) and the wave's undecided list.
 constexpr int SB32C = 512;  // 8 waves share each LDS chunk
+// 32-centre blocks per chunk: what LDS_BUDGET holds, rounded down to whole
+// packing groups of 8 (9 at NK = 4 left a one-block group and a short last
+// chunk: 8 is 1 ms faster at C3, profiles/r06/c3ab/r06zi_c32_cb8_ab.txt)
 template <int NK>
-constexpr int c32_cb() {  // 32-centre blocks per chunk within LDS_BUDGET
-  return (int)(LDS_BUDGET / (NK * 2048 + 128));
+constexpr int c32_cb() {
+  constexpr int c = (int)(LDS_BUDGET / (NK * 2048 + 128));
+  return c >= 8 ? c / 8 * 8 : c;
 }
 template <class TX, int NK>
 __global__ void __launch_bounds__(SB32C) __attribute__((amdgpu_waves_per_eu(4)))
